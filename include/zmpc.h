@@ -1,0 +1,114 @@
+/*
+ * zmpc.h — C-ABI of the MI355X batched Wieber LIPM-ZMP MPC solver (libzmpc.so).
+ *
+ * This is the drop-in boundary for the reference hot path
+ *   src/mpc_bipedal/controllers/zmp_controller.py  (ZMPController, reference @ 2025-12-26)
+ * Every entry point names the reference code it replaces.  The Python host layer
+ * (mpc_bipedal/_native.py, ctypes) binds exactly these symbols; see INTEGRATION.md.
+ *
+ * Conventions
+ *  - All array pointers are DEVICE pointers (e.g. torch tensor .data_ptr()), contiguous,
+ *    IEEE fp64 unless stated.  Nothing is copied to or from the host by the solve calls.
+ *  - Calls are asynchronous on `stream` (a hipStream_t; NULL = the null stream).
+ *  - Return 0 on success, a negative ZMPC_E* code on failure; zmpc_last_error() returns a
+ *    thread-local message for the last failure on the calling thread.  No C++ exception
+ *    crosses the ABI.
+ *  - A plan is immutable after creation and may be shared across threads and streams of
+ *    its device.
+ *  - status[b] (int32, may be NULL) receives ZMPC_OK, or a per-instance failure flag
+ *    (ZMPC_ST_*).  The reference raises RuntimeError("QP solver did not find a solution")
+ *    for a failed strict solve (zmp_controller.py:193-194); the host layer does the same
+ *    when any status is non-zero.
+ */
+#ifndef ZMPC_H
+#define ZMPC_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ZMPC_ABI_VERSION 1
+
+/* return codes */
+#define ZMPC_OK 0
+#define ZMPC_EINVAL (-1)   /* bad argument (size, pointer, range) */
+#define ZMPC_EHIP (-2)     /* HIP runtime error (message has hipGetErrorString) */
+#define ZMPC_ENOMEM (-3)   /* device allocation failed */
+#define ZMPC_ESTATE (-4)   /* plan does not support the request (e.g. strict workspace) */
+
+/* per-instance status flags (bitwise OR) */
+#define ZMPC_ST_MAXITER 1  /* strict active-set iteration cap reached */
+#define ZMPC_ST_NONFINITE 2 /* a non-finite value was produced */
+#define ZMPC_ST_FACTOR 4   /* reduced KKT matrix not positive definite */
+
+typedef struct zmpc_plan zmpc_plan;
+
+/*
+ * Build the batch-invariant solver plan on `device` (stream-ordered on `stream`, then
+ * synchronised): the Toeplitz column p of Pu and Px (zmp_controller.py:162-171, built on
+ * the device from the host-evaluated constants so they match the reference bit for bit),
+ * M = PuᵀPu + (R/Q)·I (FP64 MFMA when N >= 64, zmp_controller.py:198), its Cholesky
+ * factor, the gain row k = e0ᵀ M⁻¹ Puᵀ and kx = k·Px (the only part of
+ * -inv(M) Puᵀ (Px x - z_ref) the reference uses, X[0], zmp_controller.py:198-199) and,
+ * when strict != 0, the z-space inverse Hessian G = Pu (R·I + Q·PuᵀPu)⁻¹ Puᵀ of the
+ * strict QP (zmp_controller.py:173-195).
+ * Replaces the per-call matrix build in ZMPController.predict_wieber_axis
+ * (zmp_controller.py:162-171) and the inverse at :198.
+ *   T, T2_2 = T²/2, T3_6 = T³/6, hg = h/g, Thg = T·h/g: as Python evaluates them
+ *   (mpc_bipedal/models/lipm_model.py:plan_constants).
+ */
+int zmpc_plan_create(int device, int32_t N, double T, double T2_2, double T3_6, double hg,
+                     double Thg, double Q, double R, int32_t strict, void* stream,
+                     zmpc_plan** out);
+
+/* Release a plan (synchronises its device). */
+int zmpc_plan_destroy(zmpc_plan* plan);
+
+/* Plan quantities copied to HOST memory for inspection/tests.
+ * what: 0 = p (N), 1 = Px (N*3, row-major), 2 = M (N*N), 3 = gain k (N), 4 = kx (3),
+ *       5 = G (N*N, strict plans only), 6 = Cholesky factor L of M (N*N, lower).
+ * count = number of doubles dst can hold; must be >= the quantity's size. */
+int zmpc_plan_export(const zmpc_plan* plan, int32_t what, double* dst_host, int64_t count);
+
+/*
+ * Batched ZMPController.predict_wieber_axis (zmp_controller.py:149-201):
+ * B independent one-axis QP solves, one per instance b:
+ *   x[b] (3) state, zmax_win[b], zmin_win[b] (N) the preview window
+ *   → x_next[b] (3) = A x + B·u0, u0 = first jerk of the QP solution
+ *     (unconstrained: :196-198; strict box-QP: :173-195).
+ */
+int zmpc_step(const zmpc_plan* plan, int64_t B, const double* x, const double* zmax_win,
+              const double* zmin_win, double* x_next, int32_t* status, void* stream);
+
+/*
+ * Batched Wieber rollout: ZMPController.generate_com_trajectory_wieber
+ * (zmp_controller.py:59-108) and generate_state_trajectory_wieber (:110-147) for B walks.
+ *   zmax, zmin : [B, n, 2]   CoP bounds per walk (x, y); the window at step i is rows
+ *                            i+1 .. i+N, padded with the last row (:81-88)
+ *   bounds_stride            doubles between consecutive walks' bound arrays: 2n for a
+ *                            dense [B,n,2] batch, 0 when every walk shares one CoP
+ *                            (e.g. a disturbance sweep over one footstep plan)
+ *   x0         : [B, 2, 3]   initial (x-axis, y-axis) states
+ *   kick       : [B] or NULL velocity impulse dt·F_ext/m subtracted from the y state
+ *                            produced at step kick_step (:90,105-106); NULL = no force
+ *   hist       : [B, n, 2, 3] output state history, hist[:,0] = x0
+ * n >= 1.  The CoM trajectory of the reference is hist[:, :, :, 0].
+ */
+int zmpc_rollout(const zmpc_plan* plan, int64_t B, int64_t n, const double* zmax,
+                 const double* zmin, int64_t bounds_stride, const double* x0,
+                 const double* kick, int64_t kick_step, double* hist, int32_t* status,
+                 void* stream);
+
+/* Message describing the last failure on the calling thread ("" if none). */
+const char* zmpc_last_error(void);
+
+/* ZMPC_ABI_VERSION of the loaded library. */
+int zmpc_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ZMPC_H */

@@ -1,0 +1,229 @@
+// C-ABI of libzmpc.so (declared in include/zmpc.h).  Host-side only: argument checks,
+// device selection, buffer ownership of plans, error reporting.  No compute runs here.
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+#include "zmpc_internal.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+  return fail(ZMPC_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// Switch to the plan's device for the duration of a call, restore the caller's device.
+struct DeviceGuard {
+  int prev = -1;
+  hipError_t err = hipSuccess;
+  explicit DeviceGuard(int dev) {
+    if ((err = hipGetDevice(&prev)) != hipSuccess) return;
+    if (prev != dev) err = hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur = -1;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+void free_plan(zmpc_plan* p) {
+  if (!p) return;
+  double* bufs[] = {p->p, p->Px, p->M, p->L, p->k, p->kx, p->X, p->G};
+  for (double* b : bufs)
+    if (b) (void)hipFree(b);
+  if (p->info) (void)hipFree(p->info);
+  if (p->scratch) (void)hipFree(p->scratch);
+  delete p;
+}
+
+bool attrs_done[64] = {};
+
+}  // namespace
+
+extern "C" {
+
+int zmpc_abi_version(void) { return ZMPC_ABI_VERSION; }
+
+const char* zmpc_last_error(void) { return g_err.c_str(); }
+
+int zmpc_plan_create(int device, int32_t N, double T, double T2_2, double T3_6, double hg,
+                     double Thg, double Q, double R, int32_t strict, void* stream,
+                     zmpc_plan** out) {
+  g_err.clear();
+  if (!out) return fail(ZMPC_EINVAL, "out is NULL");
+  *out = nullptr;
+  if (N < 1 || N > 4096) return fail(ZMPC_EINVAL, "horizon N must be in [1, 4096]");
+  if (!(T > 0) || !(Q > 0) || !(R >= 0))
+    return fail(ZMPC_EINVAL, "need dt > 0, Q > 0, R >= 0");
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess) return hip_fail(e, "hipGetDeviceCount");
+  if (device < 0 || device >= ndev) return fail(ZMPC_EINVAL, "device index out of range");
+  DeviceGuard g(device);
+  if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
+  if (device < 64 && !attrs_done[device]) {
+    if ((e = zmpc_rollout_unc_set_attrs()) != hipSuccess) return hip_fail(e, "set LDS attrs");
+    if ((e = zmpc_strict_set_attrs()) != hipSuccess) return hip_fail(e, "set LDS attrs");
+    attrs_done[device] = true;
+  }
+
+  zmpc_plan* P = new zmpc_plan();
+  P->device = device;
+  P->N = N;
+  P->Kpad = (N + 15) & ~15;
+  P->strict = strict ? 1 : 0;
+  P->T = T;
+  P->T2_2 = T2_2;
+  P->T3_6 = T3_6;
+  P->hg = hg;
+  P->Thg = Thg;
+  P->Q = Q;
+  P->R = R;
+  P->lc = LipmConsts{T, T2_2, T3_6};
+  const size_t nn = (size_t)N * N;
+  struct {
+    double** ptr;
+    size_t n;
+  } allocs[] = {{&P->p, (size_t)N},  {&P->Px, 3 * (size_t)N}, {&P->M, nn}, {&P->L, nn},
+                {&P->k, (size_t)P->Kpad + 64}, {&P->kx, 4},
+                {&P->X, strict ? nn : 0}, {&P->G, strict ? nn : 0}};
+  for (auto& a : allocs) {
+    if (a.n == 0) continue;
+    if ((e = hipMalloc((void**)a.ptr, a.n * sizeof(double))) != hipSuccess) {
+      free_plan(P);
+      return fail(ZMPC_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    }
+  }
+  if ((e = hipMalloc((void**)&P->info, sizeof(int))) != hipSuccess) {
+    free_plan(P);
+    return fail(ZMPC_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+  }
+  if (strict) {
+    int cus = 0;
+    if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device)) !=
+        hipSuccess) {
+      free_plan(P);
+      return hip_fail(e, "hipDeviceGetAttribute");
+    }
+    P->strict_slots = 2 * cus;
+    const size_t bytes = (size_t)P->strict_slots * 4 * nn * sizeof(double);
+    if ((e = hipMalloc((void**)&P->scratch, bytes)) != hipSuccess) {
+      free_plan(P);
+      return fail(ZMPC_ENOMEM, std::string("hipMalloc scratch: ") + hipGetErrorString(e));
+    }
+  }
+  hipStream_t s = (hipStream_t)stream;
+  (void)hipMemsetAsync(P->k, 0, ((size_t)P->Kpad + 64) * sizeof(double), s);
+  if ((e = zmpc_launch_plan(P, s)) != hipSuccess) {
+    free_plan(P);
+    return hip_fail(e, "plan kernels");
+  }
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) {
+    free_plan(P);
+    return hip_fail(e, "plan synchronize");
+  }
+  int info = 0;
+  if ((e = hipMemcpy(&info, P->info, sizeof(int), hipMemcpyDeviceToHost)) != hipSuccess) {
+    free_plan(P);
+    return hip_fail(e, "plan info copy");
+  }
+  if (info != 0) {
+    free_plan(P);
+    return fail(ZMPC_ESTATE, "PuᵀPu + (R/Q)I is not positive definite (pivot " +
+                                 std::to_string(info) + ")");
+  }
+  *out = P;
+  return ZMPC_OK;
+}
+
+int zmpc_plan_destroy(zmpc_plan* plan) {
+  g_err.clear();
+  if (!plan) return ZMPC_OK;
+  DeviceGuard g(plan->device);
+  (void)hipDeviceSynchronize();
+  free_plan(plan);
+  return ZMPC_OK;
+}
+
+int zmpc_plan_export(const zmpc_plan* P, int32_t what, double* dst, int64_t count) {
+  g_err.clear();
+  if (!P || !dst) return fail(ZMPC_EINVAL, "NULL plan or destination");
+  const int64_t N = P->N;
+  const double* src = nullptr;
+  int64_t n = 0;
+  switch (what) {
+    case 0: src = P->p; n = N; break;
+    case 1: src = P->Px; n = 3 * N; break;
+    case 2: src = P->M; n = N * N; break;
+    case 3: src = P->k; n = N; break;
+    case 4: src = P->kx; n = 3; break;
+    case 5: src = P->G; n = P->G ? N * N : 0; break;
+    case 6: src = P->L; n = N * N; break;
+    default: return fail(ZMPC_EINVAL, "unknown export id");
+  }
+  if (!src || n == 0) return fail(ZMPC_ESTATE, "quantity not held by this plan");
+  if (count < n) return fail(ZMPC_EINVAL, "destination too small");
+  DeviceGuard g(P->device);
+  if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
+  hipError_t e = hipDeviceSynchronize();
+  if (e != hipSuccess) return hip_fail(e, "hipDeviceSynchronize");
+  e = hipMemcpy(dst, src, n * sizeof(double), hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return hip_fail(e, "hipMemcpy");
+  return ZMPC_OK;
+}
+
+int zmpc_step(const zmpc_plan* P, int64_t B, const double* x, const double* zmax_win,
+              const double* zmin_win, double* x_next, int32_t* status, void* stream) {
+  g_err.clear();
+  if (!P) return fail(ZMPC_EINVAL, "NULL plan");
+  if (B < 0) return fail(ZMPC_EINVAL, "B < 0");
+  if (B == 0) return ZMPC_OK;
+  if (!x || !zmax_win || !zmin_win || !x_next)
+    return fail(ZMPC_EINVAL, "NULL array argument");
+  if (B > (int64_t)0x7fffffff * 4) return fail(ZMPC_EINVAL, "batch too large");
+  DeviceGuard g(P->device);
+  if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
+  std::string why;
+  hipError_t e = P->strict ? zmpc_launch_step_strict(P, B, x, zmax_win, zmin_win, x_next, status,
+                                                     (hipStream_t)stream, &why)
+                           : zmpc_launch_step_unc(P, B, x, zmax_win, zmin_win, x_next, status,
+                                                  (hipStream_t)stream);
+  if (e != hipSuccess)
+    return why.empty() ? hip_fail(e, "zmpc_step launch") : fail(ZMPC_EINVAL, why);
+  return ZMPC_OK;
+}
+
+int zmpc_rollout(const zmpc_plan* P, int64_t B, int64_t n, const double* zmax,
+                 const double* zmin, int64_t bounds_stride, const double* x0,
+                 const double* kick, int64_t kick_step, double* hist, int32_t* status,
+                 void* stream) {
+  g_err.clear();
+  if (!P) return fail(ZMPC_EINVAL, "NULL plan");
+  if (B < 0 || n < 1) return fail(ZMPC_EINVAL, "need B >= 0 and n >= 1");
+  if (B == 0) return ZMPC_OK;
+  if (!zmax || !zmin || !x0 || !hist) return fail(ZMPC_EINVAL, "NULL array argument");
+  if (B > 0x7fffffff) return fail(ZMPC_EINVAL, "batch too large");
+  if (n > (1 << 24)) return fail(ZMPC_EINVAL, "walk too long");
+  if (bounds_stride != 0 && bounds_stride < 2 * n)
+    return fail(ZMPC_EINVAL, "bounds_stride must be 0 (shared CoP) or >= 2n");
+  DeviceGuard g(P->device);
+  if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
+  std::string why;
+  hipStream_t s = (hipStream_t)stream;
+  hipError_t e = P->strict ? zmpc_launch_rollout_strict(P, B, n, zmax, zmin, bounds_stride, x0, kick, kick_step,
+                                                        hist, status, s, &why)
+                           : zmpc_launch_rollout_unc(P, B, n, zmax, zmin, bounds_stride, x0, kick, kick_step,
+                                                     hist, status, s, &why);
+  if (e != hipSuccess)
+    return why.empty() ? hip_fail(e, "zmpc_rollout launch") : fail(ZMPC_EINVAL, why);
+  return ZMPC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,490 @@
+// Strict (ZMP box-constrained) Wieber QP on the device (config.strict == True).
+//
+// Reference, per axis and timestep (zmp_controller.py:173-195, solved there by cvxpy→OSQP):
+//   min_J ½Q‖Px x + Pu J − z_ref‖² + ½R‖J‖²   s.t.  z_min ≤ Px x + Pu J ≤ z_max,  u0 = J[0]
+// Pu is lower-triangular Toeplitz with p(0) ≠ 0, hence invertible: in ZMP coordinates
+// z = Px x + Pu J the constraints are simple bounds and the problem is a strictly convex
+// box-QP, always feasible.  With c = Px x and the plan's G = Pu (R·I + Q·PuᵀPu)⁻¹ Puᵀ
+// (the inverse z-space Hessian):
+//   unconstrained     z* = c + Q·G (z_ref − c)
+//   active set A      z  = z* − G ν,   ν_A = G_AA⁻¹ (z*_A − t_A),  t = bound value
+//   KKT               ν ≥ 0 on upper-active, ν ≤ 0 on lower-active, z_min ≤ z ≤ z_max on free
+//   first jerk        u0 = (z_0 − c_0) / p(0) = (D_0 − (Gν)_0) / p(0),  D = Q·G(z_ref − c)
+// The active set is found by a primal-dual active-set iteration warm-started from the
+// previous timestep's set shifted by one horizon slot (the rollout's windows slide by one).
+//
+// Mapping: a workgroup (4 waves) owns a tile of 16 instances (instance = walk × axis) for the
+// whole rollout, persistent over tiles.  Per timestep:
+//   GEMM   D[:, 16 instances] = G · W with W = Q (z_ref − c): v_mfma_f64_16x16x4_f64, G from
+//          L2 (batch-invariant, 176 KB at N=150), W/D tile in LDS;
+//   solve  each wave takes 4 instances: PDAS; G_AA Cholesky in LDS (in a per-wave global
+//          scratch when |A| is large), state advance, kick, history store, next W.
+#include "zmpc_internal.h"
+
+namespace {
+
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
+constexpr int SNB = 16;            // instances per tile (= MFMA column tile)
+constexpr int SWAVES = 4;          // waves per workgroup
+constexpr int SPW = SNB / SWAVES;  // instances per wave
+constexpr int SMAX_RT = 8;         // row tiles per wave (N <= 512)
+constexpr int SMAXIT = 64;         // PDAS iteration cap
+
+struct StrictArgs {
+  int N, Np, ld;         // horizon, padded to 16, W/D leading dimension
+  int mcap;              // largest |A| factored in LDS
+  int window_mode;       // 0 = rollout over [B,n,2] bounds, 1 = single step on [B,N] windows
+  int64_t n;             // samples per walk (rollout)
+  int64_t bstride;       // doubles between walks' bound arrays (0 = shared CoP)
+  int64_t ninst;         // instances: 2B (rollout) or B (step)
+  double Q, p0;
+  LipmConsts lc;
+  const double* G;       // [N,N]
+  const double* Px;      // [N,3]
+  const double* zmax;
+  const double* zmin;
+  const double* x0;      // rollout [B,2,3], step [B,3]
+  const double* kick;    // [B] or null
+  int64_t kick_step;
+  double* out;           // rollout hist [B,n,2,3], step x_next [B,3]
+  int32_t* status;       // [B] or null
+  double* scratch;       // per-wave N*N factor scratch (gridDim*SWAVES slots)
+};
+
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ void lipm_step(const LipmConsts& c, const double* x, double u,
+                                          double* y) {
+  y[0] = x[0] + c.T * x[1] + c.T2_2 * x[2] + c.T3_6 * u;
+  y[1] = x[1] + c.T * x[2] + c.T2_2 * u;
+  y[2] = x[2] + c.T * u;
+}
+
+// Window element j of instance `inst` at timestep i (rows i+1.., padded with the last row,
+// zmp_controller.py:81-88,97-98).
+__device__ __forceinline__ int64_t bound_index(const StrictArgs& a, int64_t inst, int64_t i,
+                                               int j) {
+  if (a.window_mode) return inst * a.N + j;
+  const int64_t b = inst >> 1, axis = inst & 1;
+  int64_t t = i + 1 + j;
+  if (t > a.n - 1) t = a.n - 1;
+  return b * a.bstride + t * 2 + axis;
+}
+
+// W[j] = Q (z_ref_j − c_j), c = Px x; zero on the padding rows.
+__device__ void build_w(const StrictArgs& a, int64_t inst, int64_t i, const double* x,
+                        double* W, int lane) {
+  for (int j = lane; j < a.Np; j += 64) {
+    double w = 0.0;
+    if (j < a.N) {
+      const int64_t e = bound_index(a, inst, i, j);
+      const double zr = (a.zmax[e] + a.zmin[e]) / 2;
+      const double c = a.Px[3 * j] * x[0] + a.Px[3 * j + 1] * x[1] + a.Px[3 * j + 2] * x[2];
+      w = a.Q * (zr - c);
+    }
+    W[j] = w;
+  }
+}
+
+// In-place lower Cholesky of the m×m matrix S (leading dimension m) by one wave.
+// Returns false if a pivot is not positive.
+__device__ bool wave_cholesky(double* S, int m, int lane) {
+  for (int k = 0; k < m; ++k) {
+    const double d = S[k * m + k];
+    if (!(d > 0.0)) return false;
+    const double piv = sqrt(d);
+    const double inv = 1.0 / piv;
+    wave_sync();
+    for (int i = k + 1 + lane; i < m; i += 64) S[i * m + k] *= inv;
+    if (lane == 0) S[k * m + k] = piv;
+    wave_sync();
+    const int r = m - k - 1;
+    for (int t = lane; t < r * r; t += 64) {
+      const int i = k + 1 + t / r, j = k + 1 + t % r;
+      if (j <= i) S[i * m + j] -= S[i * m + k] * S[j * m + k];
+    }
+    wave_sync();
+  }
+  return true;
+}
+
+// Solve (L Lᵀ) v = rhs in place (rhs in v), L from wave_cholesky.
+__device__ void wave_chol_solve(const double* S, int m, double* v, int lane) {
+  for (int j = 0; j < m; ++j) {
+    const double yj = v[j] / S[j * m + j];
+    wave_sync();
+    for (int i = j + 1 + lane; i < m; i += 64) v[i] -= S[i * m + j] * yj;
+    if (lane == 0) v[j] = yj;
+    wave_sync();
+  }
+  for (int j = m - 1; j >= 0; --j) {
+    const double yj = v[j] / S[j * m + j];
+    wave_sync();
+    for (int i = lane; i < j; i += 64) v[i] -= S[j * m + i] * yj;
+    if (lane == 0) v[j] = yj;
+    wave_sync();
+  }
+}
+
+struct WaveWork {
+  double* zs;    // [Np] unconstrained z* − c  (= D)
+  double* zz;    // [Np] current z − c
+  double* lo;    // [Np] z_min − c
+  double* hi;    // [Np] z_max − c
+  double* nuf;   // [Np] multipliers scattered to horizon slots
+  double* nuc;   // [Np] compact right-hand side / multipliers
+  int* idx;      // [Np] compact active indices
+  double* S;     // [mcap*mcap] LDS factor workspace
+  double* Sg;    // [N*N] global factor scratch
+};
+
+constexpr int SNJ = 8;  // horizon slots per lane (N <= 512)
+
+// One strict QP solve for one instance.  D holds Q·G(z_ref − c) on entry; st is the
+// instance's warm-start status array (0 free, 1 upper, 2 lower), updated in place.
+// Returns u0 and ORs failure flags into *flags.
+__device__ double solve_instance(const StrictArgs& a, int64_t inst, int64_t i, const double* x,
+                                 const double* D, signed char* st, const WaveWork& w, int lane,
+                                 int* flags) {
+  const int N = a.N;
+  for (int j = lane; j < N; j += 64) {
+    const int64_t e = bound_index(a, inst, i, j);
+    const double c = a.Px[3 * j] * x[0] + a.Px[3 * j + 1] * x[1] + a.Px[3 * j + 2] * x[2];
+    // bounds relative to c: z − c is the working variable (u0 needs z_0 − c_0)
+    w.hi[j] = a.zmax[e] - c;
+    w.lo[j] = a.zmin[e] - c;
+    w.zs[j] = D[j];
+    w.zz[j] = D[j];
+    w.nuf[j] = 0.0;
+  }
+  wave_sync();
+  const double tolz = 1e-13, tolnu = 1e-13;
+  bool done = false;
+  for (int it = 0; it < SMAXIT; ++it) {
+    // compact the active set
+    int m = 0;
+    for (int j0 = 0; j0 < N; j0 += 64) {
+      const int j = j0 + lane;
+      const bool act = (j < N) && st[j] != 0;
+      const unsigned long long bal = __ballot(act);
+      const int pos = m + __popcll(bal & ((1ull << lane) - 1ull));
+      if (act) w.idx[pos] = j;
+      m += __popcll(bal);
+    }
+    wave_sync();
+    if (m > 0) {
+      double* S = (m <= a.mcap) ? w.S : w.Sg;
+      for (int t = lane; t < m * m; t += 64) {
+        const int r = t / m, c = t % m;
+        S[t] = a.G[(size_t)w.idx[r] * N + w.idx[c]];
+      }
+      for (int r = lane; r < m; r += 64) {
+        const int j = w.idx[r];
+        w.nuc[r] = w.zs[j] - (st[j] == 1 ? w.hi[j] : w.lo[j]);
+      }
+      wave_sync();
+      if (!wave_cholesky(S, m, lane)) {
+        *flags |= ZMPC_ST_FACTOR;
+        break;
+      }
+      wave_chol_solve(S, m, w.nuc, lane);
+      for (int r = lane; r < m; r += 64) w.nuf[w.idx[r]] = w.nuc[r];
+      // z − c = D − G_{:,A} ν_A   (G symmetric: row idx_r is column idx_r)
+      for (int j = lane; j < N; j += 64) {
+        double s = w.zs[j];
+        for (int r = 0; r < m; ++r) s -= a.G[(size_t)w.idx[r] * N + j] * w.nuc[r];
+        w.zz[j] = s;
+      }
+    } else {
+      for (int j = lane; j < N; j += 64) w.zz[j] = w.zs[j];
+    }
+    wave_sync();
+    // primal-dual set update: release active slots with wrong-signed multipliers, activate
+    // violated free slots
+    signed char ns[SNJ];
+    bool changed = false;
+#pragma unroll
+    for (int c = 0; c < SNJ; ++c) {
+      const int j = lane + 64 * c;
+      ns[c] = 0;
+      if (j < N) {
+        const signed char o = st[j];
+        signed char v = o;
+        if (o == 1) {
+          if (w.nuf[j] < -tolnu) v = 0;
+        } else if (o == 2) {
+          if (w.nuf[j] > tolnu) v = 0;
+        } else if (w.zz[j] > w.hi[j] + tolz) {
+          v = 1;
+        } else if (w.zz[j] < w.lo[j] - tolz) {
+          v = 2;
+        }
+        ns[c] = v;
+        changed |= (v != o);
+      }
+    }
+    changed = __any(changed);
+    if (!changed) {
+      done = true;
+      break;
+    }
+#pragma unroll
+    for (int c = 0; c < SNJ; ++c) {
+      const int j = lane + 64 * c;
+      if (j < N) {
+        st[j] = ns[c];
+        w.nuf[j] = 0.0;
+      }
+    }
+    wave_sync();
+  }
+  if (!done) *flags |= ZMPC_ST_MAXITER;
+  const double u0 = w.zz[0] / a.p0;
+  wave_sync();
+  return u0;
+}
+
+__global__ void __launch_bounds__(256) zmpc_strict_kernel(StrictArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int Np = a.Np, ld = a.ld;
+  // LDS carve: Wt [SNB][ld] | xs [SNB][4] | flags [SNB] (as doubles) |
+  //            per wave {zs,zz,lo,hi,nuf,nuc}[Np], idx[Np] ints, S[mcap²] | st [SNB][Np] bytes
+  double* Wt = smem;
+  double* xs = Wt + SNB * ld;
+  int* fl = reinterpret_cast<int*>(xs + SNB * 4);
+  double* wbase = xs + SNB * 4 + SNB;
+  const int per_wave = 6 * Np + Np / 2 + a.mcap * a.mcap;
+  double* my = wbase + wave * per_wave;
+  WaveWork w;
+  w.zs = my;
+  w.zz = my + Np;
+  w.lo = my + 2 * Np;
+  w.hi = my + 3 * Np;
+  w.nuf = my + 4 * Np;
+  w.nuc = my + 5 * Np;
+  w.idx = reinterpret_cast<int*>(my + 6 * Np);
+  w.S = my + 6 * Np + Np / 2;
+  w.Sg = a.scratch + ((size_t)blockIdx.x * SWAVES + wave) * (size_t)a.N * a.N;
+  signed char* stall = reinterpret_cast<signed char*>(wbase + SWAVES * per_wave);
+
+  const int64_t ntiles = (a.ninst + SNB - 1) / SNB;
+  const int64_t nsteps = a.window_mode ? 1 : a.n - 1;
+  const int nrt = Np / 16;
+
+  for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    // ---- tile setup: states, warm-start sets, first W --------------------------------
+    for (int q = 0; q < SPW; ++q) {
+      const int s = wave * SPW + q;
+      const int64_t inst = tile * SNB + s;
+      double* x = xs + s * 4;
+      signed char* st = stall + s * Np;
+      for (int j = lane; j < Np; j += 64) st[j] = 0;
+      if (lane == 0) fl[s] = 0;
+      if (lane < 3) x[lane] = (inst < a.ninst) ? a.x0[inst * 3 + lane] : 0.0;
+      wave_sync();
+      if (!a.window_mode && inst < a.ninst && lane < 3) {
+        // hist[b, 0, axis, :] = x0
+        a.out[((inst >> 1) * a.n * 2 + (inst & 1)) * 3 + lane] = x[lane];
+      }
+      if (inst < a.ninst)
+        build_w(a, inst, 0, x, Wt + s * ld, lane);
+      else
+        for (int j = lane; j < ld; j += 64) Wt[s * ld + j] = 0.0;
+    }
+    __syncthreads();
+
+    for (int64_t i = 0; i < nsteps; ++i) {
+      // ---- GEMM: D = G · W for the 16 instances of the tile (MFMA f64) ----------------
+      dbl4 acc[SMAX_RT];
+#pragma unroll
+      for (int t = 0; t < SMAX_RT; ++t) acc[t] = dbl4{0.0, 0.0, 0.0, 0.0};
+      {
+        const int r = lane & 15, kq = lane >> 4;
+#pragma unroll
+        for (int t = 0; t < SMAX_RT; ++t) {
+          const int rt = wave + SWAVES * t;
+          if (rt < nrt) {
+            const int row = rt * 16 + r;
+            for (int k0 = 0; k0 < Np; k0 += 4) {
+              const int k = k0 + kq;
+              const double gv = (row < a.N && k < a.N) ? a.G[(size_t)k * a.N + row] : 0.0;
+              const double wv = Wt[r * ld + k];
+              acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(gv, wv, acc[t], 0, 0, 0);
+            }
+          }
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int t = 0; t < SMAX_RT; ++t) {
+        const int rt = wave + SWAVES * t;
+        if (rt < nrt) {
+          const int col = lane & 15;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) Wt[col * ld + rt * 16 + (lane >> 4) + 4 * q] = acc[t][q];
+        }
+      }
+      __syncthreads();
+
+      // ---- per-instance active set, state advance, next W ------------------------------
+      for (int q = 0; q < SPW; ++q) {
+        const int s = wave * SPW + q;
+        const int64_t inst = tile * SNB + s;
+        if (inst >= a.ninst) continue;
+        double* x = xs + s * 4;
+        signed char* st = stall + s * Np;
+        const double xv[3] = {x[0], x[1], x[2]};
+        // warm start: shift the previous set one slot towards the present
+        if (i > 0) {
+          signed char v[SNJ];
+#pragma unroll
+          for (int c = 0; c < SNJ; ++c) {
+            const int j = lane + 64 * c;
+            v[c] = (j + 1 < a.N) ? st[j + 1] : ((j < a.N) ? st[j] : 0);
+          }
+          wave_sync();
+#pragma unroll
+          for (int c = 0; c < SNJ; ++c)
+            if (lane + 64 * c < a.N) st[lane + 64 * c] = v[c];
+          wave_sync();
+        }
+        int fq = 0;
+        const double u0 = solve_instance(a, inst, i, xv, Wt + s * ld, st, w, lane, &fq);
+        double xn[3];
+        lipm_step(a.lc, xv, u0, xn);
+        if (!a.window_mode && (inst & 1) && i == a.kick_step && a.kick != nullptr)
+          xn[1] -= a.kick[inst >> 1];
+        if (!(isfinite(xn[0]) && isfinite(xn[1]) && isfinite(xn[2]))) fq |= ZMPC_ST_NONFINITE;
+        if (lane == 0) fl[s] |= fq;
+        wave_sync();
+        if (lane < 3) x[lane] = xn[lane];
+        if (a.window_mode) {
+          if (lane < 3) a.out[inst * 3 + lane] = xn[lane];
+        } else if (lane < 3) {
+          a.out[(((inst >> 1) * a.n + i + 1) * 2 + (inst & 1)) * 3 + lane] = xn[lane];
+        }
+        wave_sync();
+        if (i + 1 < nsteps) build_w(a, inst, i + 1, xn, Wt + s * ld, lane);
+      }
+      __syncthreads();
+    }
+    // ---- status: OR over the axes of a walk -------------------------------------------
+    if (a.status != nullptr) {
+      for (int q = 0; q < SPW; ++q) {
+        const int s = wave * SPW + q;
+        const int64_t inst = tile * SNB + s;
+        if (inst < a.ninst && lane == 0) {
+          if (a.window_mode)
+            a.status[inst] = fl[s];
+          else if (fl[s] != 0)
+            atomicOr(&a.status[inst >> 1], fl[s]);
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+size_t strict_lds_bytes(int Np, int ld, int mcap) {
+  const size_t per_wave = 6 * Np + Np / 2 + (size_t)mcap * mcap;
+  return (SNB * ld + SNB * 4 + SNB + SWAVES * per_wave) * sizeof(double) + SNB * Np;
+}
+
+}  // namespace
+
+hipError_t zmpc_strict_set_attrs() {
+  return hipFuncSetAttribute((const void*)zmpc_strict_kernel,
+                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+}
+
+static hipError_t launch_strict(const zmpc_plan* p, StrictArgs a, hipStream_t s,
+                                std::string* why) {
+  if (p->N > 16 * SWAVES * SMAX_RT) {
+    *why = "strict solver supports horizon N <= " + std::to_string(16 * SWAVES * SMAX_RT);
+    return hipErrorInvalidValue;
+  }
+  a.N = p->N;
+  a.Np = (p->N + 15) & ~15;
+  a.ld = a.Np + 4;
+  int mcap = 48;
+  while (mcap > 0 && strict_lds_bytes(a.Np, a.ld, mcap) > 150 * 1024) mcap -= 8;
+  if (strict_lds_bytes(a.Np, a.ld, mcap) > 160 * 1024) {
+    *why = "horizon too long for the strict solver's LDS tile (N=" + std::to_string(p->N) + ")";
+    return hipErrorInvalidValue;
+  }
+  a.mcap = mcap;
+  a.Q = p->Q;
+  a.lc = p->lc;
+  a.G = p->G;
+  a.Px = p->Px;
+  // p(0) = T³/6·1 − T h/g  (zmp_controller.py:171 with i = j)
+  a.p0 = p->T3_6 - p->Thg;
+  const int64_t ntiles = (a.ninst + SNB - 1) / SNB;
+  int grid = (int)std::min<int64_t>(ntiles, (int64_t)p->strict_slots);
+  a.scratch = p->scratch;
+  const size_t lds = strict_lds_bytes(a.Np, a.ld, a.mcap);
+  hipLaunchKernelGGL(zmpc_strict_kernel, dim3(grid), dim3(256), lds, s, a);
+  return hipGetLastError();
+}
+
+hipError_t zmpc_launch_rollout_strict(const zmpc_plan* p, int64_t B, int64_t n,
+                                      const double* zmax, const double* zmin, int64_t bstride,
+                                      const double* x0,
+                                      const double* kick, int64_t kick_step, double* hist,
+                                      int32_t* status, hipStream_t s, std::string* why) {
+  if (!p->G) {
+    *why = "plan was created without strict workspace";
+    return hipErrorInvalidValue;
+  }
+  if (n == 1) {
+    hipError_t e = hipMemcpyAsync(hist, x0, 6 * sizeof(double) * (size_t)B,
+                                  hipMemcpyDeviceToDevice, s);
+    if (e != hipSuccess) return e;
+    if (status) return hipMemsetAsync(status, 0, sizeof(int32_t) * B, s);
+    return hipSuccess;
+  }
+  if (status) {
+    hipError_t e = hipMemsetAsync(status, 0, sizeof(int32_t) * B, s);
+    if (e != hipSuccess) return e;
+  }
+  StrictArgs a{};
+  a.window_mode = 0;
+  a.n = n;
+  a.bstride = bstride;
+  a.ninst = 2 * B;
+  a.zmax = zmax;
+  a.zmin = zmin;
+  a.x0 = x0;
+  a.kick = kick;
+  a.kick_step = kick_step;
+  a.out = hist;
+  a.status = status;
+  return launch_strict(p, a, s, why);
+}
+
+hipError_t zmpc_launch_step_strict(const zmpc_plan* p, int64_t B, const double* x,
+                                   const double* zmax_win, const double* zmin_win,
+                                   double* x_next, int32_t* status, hipStream_t s,
+                                   std::string* why) {
+  if (!p->G) {
+    *why = "plan was created without strict workspace";
+    return hipErrorInvalidValue;
+  }
+  StrictArgs a{};
+  a.window_mode = 1;
+  a.n = 0;
+  a.ninst = B;
+  a.zmax = zmax_win;
+  a.zmin = zmin_win;
+  a.x0 = x;
+  a.kick = nullptr;
+  a.kick_step = -1;
+  a.out = x_next;
+  a.status = status;
+  return launch_strict(p, a, s, why);
+}

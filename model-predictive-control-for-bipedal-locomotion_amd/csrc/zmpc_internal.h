@@ -1,0 +1,69 @@
+// Internal declarations shared by the HIP translation units of libzmpc.so.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "zmpc.h"
+
+// Scalar LIPM constants of zmp_controller.py:18-20 (A = [[1,T,T²/2],[0,1,T],[0,0,1]],
+// B = [T³/6, T²/2, T]ᵀ), evaluated on the host as Python evaluates them.
+struct LipmConsts {
+  double T;     // A[0,1] = A[1,2] = B[2]
+  double T2_2;  // A[0,2] = B[1]
+  double T3_6;  // B[0]
+};
+
+struct zmpc_plan {
+  int device = 0;
+  int N = 0;        // horizon (nb_steps)
+  int Kpad = 0;     // N rounded up to a multiple of 16, the zero-padded length of k
+  int strict = 0;
+  double T = 0, T2_2 = 0, T3_6 = 0, hg = 0, Thg = 0, Q = 1, R = 0;
+  LipmConsts lc{};
+  // device buffers
+  double* p = nullptr;   // [N] Toeplitz column of Pu
+  double* Px = nullptr;  // [N,3]
+  double* M = nullptr;   // [N,N] PuᵀPu + (R/Q) I
+  double* L = nullptr;   // [N,N] lower Cholesky factor of M
+  double* k = nullptr;   // [Kpad] gain row e0ᵀ M⁻¹ Puᵀ (zero-padded)
+  double* kx = nullptr;  // [3]  k·Px
+  double* X = nullptr;   // [N,N] L⁻¹ Puᵀ (strict plans)
+  double* G = nullptr;   // [N,N] Pu (R I + Q PuᵀPu)⁻¹ Puᵀ (strict plans)
+  int* info = nullptr;   // [1] factorisation status
+  // strict solver: persistent-grid slots and their per-wave factor scratch
+  int strict_slots = 0;
+  double* scratch = nullptr;  // [strict_slots * 4 * N * N]
+};
+
+// kernels launchers (plan.hip)
+hipError_t zmpc_launch_plan(zmpc_plan* p, hipStream_t s);
+
+// unconstrained rollout / step (rollout.hip)
+hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, const double* zmax,
+                                   const double* zmin, int64_t bstride, const double* x0,
+                                   const double* kick,
+                                   int64_t kick_step, double* hist, int32_t* status,
+                                   hipStream_t s, std::string* why);
+hipError_t zmpc_launch_step_unc(const zmpc_plan* p, int64_t B, const double* x,
+                                const double* zmax_win, const double* zmin_win, double* x_next,
+                                int32_t* status, hipStream_t s);
+
+// strict box-QP rollout / step (strict.hip)
+hipError_t zmpc_launch_rollout_strict(const zmpc_plan* p, int64_t B, int64_t n,
+                                      const double* zmax, const double* zmin, int64_t bstride,
+                                      const double* x0,
+                                      const double* kick, int64_t kick_step, double* hist,
+                                      int32_t* status, hipStream_t s, std::string* why);
+hipError_t zmpc_launch_step_strict(const zmpc_plan* p, int64_t B, const double* x,
+                                   const double* zmax_win, const double* zmin_win,
+                                   double* x_next, int32_t* status, hipStream_t s,
+                                   std::string* why);
+
+hipError_t zmpc_rollout_unc_set_attrs();
+hipError_t zmpc_strict_set_attrs();
+
+// Dynamic LDS the rollout kernel needs for (N, n); 0 if it does not fit a CU.
+size_t zmpc_rollout_unc_lds_bytes(int Kpad, int64_t n);

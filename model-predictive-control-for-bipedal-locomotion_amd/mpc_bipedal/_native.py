@@ -1,0 +1,81 @@
+"""ctypes binding of libzmpc.so, the C-ABI declared in ``include/zmpc.h``.
+
+This is the only door to the solver: there is no CPU fallback.  If the shared library is
+missing or a HIP device is absent, every solver entry point raises instead of computing
+something else.
+"""
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("ZMPC_LIB", os.path.join(_HERE, "libzmpc.so"))
+
+ZMPC_OK = 0
+ZMPC_EINVAL = -1
+ZMPC_EHIP = -2
+ZMPC_ENOMEM = -3
+ZMPC_ESTATE = -4
+
+ST_MAXITER = 1
+ST_NONFINITE = 2
+ST_FACTOR = 4
+
+EXPORT_P, EXPORT_PX, EXPORT_M, EXPORT_K, EXPORT_KX, EXPORT_G, EXPORT_L = range(7)
+
+# every symbol include/zmpc.h declares, with (restype, argtypes)
+_c_dbl_p = ctypes.c_void_p  # device pointers travel as integers
+SIGNATURES = {
+    "zmpc_abi_version": (ctypes.c_int, []),
+    "zmpc_last_error": (ctypes.c_char_p, []),
+    "zmpc_plan_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int32, ctypes.c_double,
+                                        ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                        ctypes.c_double, ctypes.c_double, ctypes.c_double,
+                                        ctypes.c_int32, ctypes.c_void_p,
+                                        ctypes.POINTER(ctypes.c_void_p)]),
+    "zmpc_plan_destroy": (ctypes.c_int, [ctypes.c_void_p]),
+    "zmpc_plan_export": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32,
+                                        ctypes.POINTER(ctypes.c_double), ctypes.c_int64]),
+    "zmpc_step": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, _c_dbl_p, _c_dbl_p, _c_dbl_p,
+                                 _c_dbl_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "zmpc_rollout": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, _c_dbl_p,
+                                    _c_dbl_p, ctypes.c_int64, _c_dbl_p, _c_dbl_p, ctypes.c_int64,
+                                    _c_dbl_p, ctypes.c_void_p, ctypes.c_void_p]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+class NativeError(RuntimeError):
+    """A libzmpc call failed (message from zmpc_last_error)."""
+
+
+def load():
+    """Load libzmpc.so once; raise with a build hint if it is not there."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise NativeError(
+                f"libzmpc.so not found at {LIB_PATH}: build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (or `make -C "
+                "model-predictive-control-for-bipedal-locomotion_amd/csrc`).  There is no CPU "
+                "fallback for the solver.")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
+
+
+def check(rc: int, what: str):
+    if rc != ZMPC_OK:
+        msg = load().zmpc_last_error().decode(errors="replace")
+        if rc == ZMPC_EINVAL:
+            raise ValueError(f"{what}: {msg}")
+        raise NativeError(f"{what} failed ({rc}): {msg}")

@@ -1,0 +1,176 @@
+"""Zero Moment Point (ZMP) controller using Model Predictive Control — HIP device path.
+
+Drop-in for the reference ``ZMPController`` (``src/mpc_bipedal/controllers/zmp_controller.py``):
+same constructor, same attributes (``config``, ``A``, ``B``, ``C``, ``external_force``), same
+method names, argument meanings, shapes, return values and errors for the Wieber path.  Every
+QP solve runs in hand-written HIP kernels (``csrc/``) reached through the C-ABI of
+``include/zmpc.h``; NumPy inputs are staged to the device and results copied back, which is
+the only host work.  There is no CPU solver behind this class.
+
+Additions (not in the reference): ``generate_com_trajectory_batch`` /
+``generate_state_trajectory_batch`` for many walks or disturbance scenarios at once, taking
+and returning torch device tensors.
+"""
+
+from typing import Optional, Tuple
+
+import numpy as np
+import torch
+
+from ..config import MPCConfig
+from ..models.lipm_model import lipm_matrices
+from ..solver import get_plan
+
+_FAILED = "QP solver did not find a solution (infeasible or other)."
+
+
+class ZMPController:
+    """ZMP Controller using Model Predictive Control for bipedal locomotion."""
+
+    def __init__(self, config: MPCConfig):
+        # zmp_controller.py:15-21
+        self.config = config
+        self.A, self.B, self.C = lipm_matrices(config.dt, config.h, config.g)
+        self.external_force = True
+
+    # ------------------------------------------------------------------ plans / helpers
+    def _plan(self, horizon: Optional[int] = None):
+        cfg = self.config
+        if horizon is not None and int(horizon) != int(cfg.horizon):
+            # predict_wieber_axis takes nb_steps explicitly (zmp_controller.py:149)
+            from dataclasses import replace
+            cfg = replace(cfg, horizon=int(horizon), dt=cfg.dt)
+        return get_plan(cfg)
+
+    def _raise_on_status(self, status):
+        if int(status.max().item() if status.numel() else 0) != 0:
+            raise RuntimeError(_FAILED)
+
+    def _kick(self) -> float:
+        # zmp_controller.py:106: dt * F_ext / m, subtracted from the y velocity
+        return self.config.dt * self.config.F_ext / self.config.m
+
+    # ------------------------------------------------------------------ reference API
+    def generate_com_trajectory(self, x_init: np.ndarray, y_init: np.ndarray,
+                                z_max: np.ndarray = None, z_min: np.ndarray = None,
+                                v_ref: np.ndarray = None, state_ref: np.ndarray = None,
+                                ) -> Tuple[np.ndarray, np.ndarray]:
+        """Route on ``config.method`` (zmp_controller.py:23-57)."""
+        method = self.config.method.lower()
+        if method == "wieber":
+            if z_max is None or z_min is None:
+                raise ValueError("z_max and z_min are required for wieber method")
+            return self.generate_com_trajectory_wieber(x_init, y_init, z_max, z_min)
+        elif method == "herdt":
+            if v_ref is None or state_ref is None:
+                raise ValueError("v_ref and state_ref are required for herdt method")
+            return self.generate_com_trajectory_herdt(x_init, y_init, v_ref, state_ref)
+        else:
+            raise ValueError(f"Unknown method: {method}. Must be 'wieber' or 'herdt'")
+
+    def generate_com_trajectory_wieber(self, x_init: np.ndarray, y_init: np.ndarray,
+                                       z_max: np.ndarray, z_min: np.ndarray
+                                       ) -> Tuple[np.ndarray, np.ndarray]:
+        """COM trajectory (n,2) and y state history (n,3,1) (zmp_controller.py:59-108)."""
+        z_max = np.asarray(z_max, dtype=np.float64)
+        z_min = np.asarray(z_min, dtype=np.float64)
+        n_steps = len(z_min)
+        force_time = n_steps // 2
+        print(f"Time of the external force: {(force_time*self.config.dt):.2f}s")
+        hist = self._rollout_host(x_init, y_init, z_max, z_min,
+                                  self._kick() if self.config.add_force else None, force_time)
+        com = hist[:, :, 0].copy()
+        y_hist = hist[:, 1, :].reshape(n_steps, 3, 1).copy()
+        return com, y_hist
+
+    def generate_state_trajectory_wieber(self, x_init: np.ndarray, y_init: np.ndarray,
+                                         z_max: np.ndarray, z_min: np.ndarray
+                                         ) -> Tuple[np.ndarray, np.ndarray]:
+        """Full x and y state histories (n,3,1) each, no force (zmp_controller.py:110-147)."""
+        z_max = np.asarray(z_max, dtype=np.float64)
+        z_min = np.asarray(z_min, dtype=np.float64)
+        n_steps = len(z_min)
+        hist = self._rollout_host(x_init, y_init, z_max, z_min, None, -1)
+        return (hist[:, 0, :].reshape(n_steps, 3, 1).copy(),
+                hist[:, 1, :].reshape(n_steps, 3, 1).copy())
+
+    def predict_wieber_axis(self, x_init: np.ndarray, nb_steps: int, z_max: np.ndarray,
+                            z_min: np.ndarray) -> np.ndarray:
+        """One-axis next state (3,1) after the first optimal jerk (zmp_controller.py:149-201)."""
+        plan = self._plan(nb_steps)
+        x = np.asarray(x_init, dtype=np.float64).reshape(1, 3)
+        zx = np.asarray(z_max, dtype=np.float64).reshape(1, -1)
+        zn = np.asarray(z_min, dtype=np.float64).reshape(1, -1)
+        if zx.shape[1] != nb_steps or zn.shape[1] != nb_steps:
+            raise ValueError(f"z_max/z_min must hold nb_steps={nb_steps} rows")
+        out, st = plan.step(x, zx, zn)
+        if plan.strict:
+            self._raise_on_status(st)
+        return out.cpu().numpy().reshape(3, 1)
+
+    # ------------------------------------------------------------------ Herdt (out of scope)
+    def generate_com_trajectory_herdt(self, *args, **kwargs):
+        """Herdt joint footstep QP (zmp_controller.py:435-531): not part of this solver."""
+        raise NotImplementedError("method='herdt' is not implemented by the HIP solver "
+                                  "(only the Wieber QP is accelerated)")
+
+    def predict_herdt_joint(self, *args, **kwargs):
+        raise NotImplementedError("method='herdt' is not implemented by the HIP solver")
+
+    # ------------------------------------------------------------------ batched additions
+    def generate_state_trajectory_batch(self, x_init, z_max, z_min, F_ext=None,
+                                        force_step: Optional[int] = None):
+        """Many walks at once; every input may be NumPy or a torch tensor.
+
+        x_init : [B,2,3] initial (x-axis, y-axis) states, or None for zeros
+        z_max, z_min : [B,n,2] per-walk CoP bounds, or [n,2] one CoP for every walk
+        F_ext : None (no disturbance) or [B] forces in N; the y velocity at history index
+                force_step+1 drops by dt·F_ext/m (default force_step = n//2, as
+                zmp_controller.py:90,105-106)
+        Returns (hist [B,n,2,3], status [B]) on the plan's device.
+        """
+        plan = self._plan()
+        dev = torch.device("cuda", plan.device)
+        zmax_t = torch.as_tensor(z_max, dtype=torch.float64, device=dev)
+        n = int(zmax_t.shape[-2])
+        if x_init is None:
+            B = 1 if zmax_t.dim() == 2 else int(zmax_t.shape[0])
+            x0 = torch.zeros((B, 2, 3), dtype=torch.float64, device=dev)
+        else:
+            x0 = torch.as_tensor(x_init, dtype=torch.float64, device=dev)
+            B = int(x0.shape[0])
+        kick = None
+        if F_ext is not None:
+            F = torch.as_tensor(F_ext, dtype=torch.float64, device=dev).reshape(B)
+            kick = self.config.dt * F / self.config.m
+        step = (n // 2) if force_step is None else int(force_step)
+        hist, st = plan.rollout(zmax_t, z_min, x0, kick=kick, kick_step=step)
+        if plan.strict:
+            self._raise_on_status(st)
+        return hist, st
+
+    def generate_com_trajectory_batch(self, x_init, z_max, z_min, F_ext=None,
+                                      force_step: Optional[int] = None):
+        """Batched generate_com_trajectory_wieber: (com [B,n,2], hist [B,n,2,3]) on device."""
+        hist, _ = self.generate_state_trajectory_batch(x_init, z_max, z_min, F_ext, force_step)
+        return hist[..., 0], hist
+
+    def zmp(self, hist):
+        """ZMP estimate C·state (run_mpc.py:294) for a [..., 3] state tensor or array."""
+        C = self.C
+        if isinstance(hist, torch.Tensor):
+            return hist @ torch.as_tensor(C, dtype=hist.dtype, device=hist.device)
+        return np.asarray(hist) @ C
+
+    # ------------------------------------------------------------------ internals
+    def _rollout_host(self, x_init, y_init, z_max, z_min, kick, kick_step) -> np.ndarray:
+        if z_max.ndim != 2 or z_max.shape[1] != 2 or z_min.shape != z_max.shape:
+            raise ValueError("z_max and z_min must both be [n_steps, 2]")
+        plan = self._plan()
+        x0 = np.stack([np.asarray(x_init, dtype=np.float64).reshape(3),
+                       np.asarray(y_init, dtype=np.float64).reshape(3)])[None]
+        kick_arr = None if kick is None else np.array([kick], dtype=np.float64)
+        hist, st = plan.rollout(z_max[None], z_min[None], x0, kick=kick_arr, kick_step=kick_step)
+        if plan.strict:
+            self._raise_on_status(st)
+        return hist[0].cpu().numpy()

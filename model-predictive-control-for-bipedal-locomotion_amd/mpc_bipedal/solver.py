@@ -1,0 +1,174 @@
+"""Device-side solver objects on top of the C-ABI (``include/zmpc.h``).
+
+``Plan`` owns one ``zmpc_plan`` (batch-invariant matrices on one HIP device).  Its methods
+take torch tensors that live on that device (PyTorch-ROCm is used for device buffers and
+streams only) and launch the HIP kernels on torch's current stream.
+"""
+
+import ctypes
+import weakref
+
+import numpy as np
+import torch
+
+from . import _native
+from .models.lipm_model import plan_constants
+
+_PLAN_CACHE = {}
+
+
+def _device_index(backend: str) -> int:
+    if not torch.cuda.is_available():
+        raise RuntimeError("the ZMP-MPC solver needs a HIP device (torch.cuda.is_available() is "
+                           "False); there is no CPU fallback")
+    if backend in ("hip", "cuda", None):
+        return torch.cuda.current_device()
+    for prefix in ("hip:", "cuda:"):
+        if backend.startswith(prefix):
+            return int(backend[len(prefix):])
+    raise ValueError(f"unknown backend {backend!r} (expected 'hip' or 'hip:<index>')")
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+class Plan:
+    """Batch-invariant solver plan for one (N, dt, h, g, Q, R, strict) on one device."""
+
+    def __init__(self, device: int, N: int, dt: float, h: float, g: float, Q: float, R: float,
+                 strict: bool):
+        lib = _native.load()
+        self.device = int(device)
+        self.N = int(N)
+        self.dt, self.h, self.g, self.Q, self.R = float(dt), float(h), float(g), float(Q), float(R)
+        self.strict = bool(strict)
+        c = plan_constants(self.dt, self.h, self.g)
+        self.consts = c
+        handle = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+            rc = lib.zmpc_plan_create(self.device, self.N, c["T"], c["T2_2"], c["T3_6"], c["hg"],
+                                      c["Thg"], self.Q, self.R, int(self.strict),
+                                      ctypes.c_void_p(stream), ctypes.byref(handle))
+        _native.check(rc, "zmpc_plan_create")
+        self._h = handle
+        self._finalizer = weakref.finalize(self, lib.zmpc_plan_destroy, handle)
+
+    @property
+    def handle(self):
+        return self._h
+
+    def export(self, what: int) -> np.ndarray:
+        n = {0: self.N, 1: 3 * self.N, 2: self.N ** 2, 3: self.N, 4: 3, 5: self.N ** 2,
+             6: self.N ** 2}[what]
+        buf = np.empty(n, dtype=np.float64)
+        rc = _native.load().zmpc_plan_export(
+            self._h, what, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), n)
+        _native.check(rc, "zmpc_plan_export")
+        if what in (1,):
+            return buf.reshape(self.N, 3)
+        if what in (2, 5, 6):
+            return buf.reshape(self.N, self.N)
+        return buf
+
+    # -- launches --------------------------------------------------------------------------
+    def _dev(self):
+        return torch.device("cuda", self.device)
+
+    def _as_dev(self, a, shape=None):
+        t = torch.as_tensor(a, dtype=torch.float64, device=self._dev())
+        t = t.contiguous()
+        if shape is not None and tuple(t.shape) != tuple(shape):
+            raise ValueError(f"expected shape {tuple(shape)}, got {tuple(t.shape)}")
+        return t
+
+    def step(self, x, zmax_win, zmin_win, status=None):
+        """Batched predict_wieber_axis: x [B,3], windows [B,N] → x_next [B,3] (device)."""
+        x = self._as_dev(x)
+        B = x.shape[0]
+        zmax_win = self._as_dev(zmax_win, (B, self.N))
+        zmin_win = self._as_dev(zmin_win, (B, self.N))
+        x = x.reshape(B, 3)
+        out = torch.empty((B, 3), dtype=torch.float64, device=self._dev())
+        st = status if status is not None else torch.empty(B, dtype=torch.int32,
+                                                           device=self._dev())
+        with torch.cuda.device(self.device):
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+            rc = _native.load().zmpc_step(self._h, B, _ptr(x), _ptr(zmax_win), _ptr(zmin_win),
+                                          _ptr(out), _ptr(st), ctypes.c_void_p(stream))
+        _native.check(rc, "zmpc_step")
+        return out, st
+
+    def rollout_launcher(self, zmax, zmin, x0, kick=None, kick_step=-1, hist=None, status=None):
+        """Validate once and return a zero-argument callable that re-issues the same rollout
+        launch on the current stream (one ctypes call, no tensor checks): for timing loops
+        and graph capture.  The tensors must stay alive while the launcher is used."""
+        hist, status, (args, keep) = self._rollout_args(zmax, zmin, x0, kick, kick_step, hist,
+                                                        status)
+        fn = _native.load().zmpc_rollout
+        dev = self.device
+
+        def launch():
+            stream = torch.cuda.current_stream(dev).cuda_stream
+            rc = fn(*args, ctypes.c_void_p(stream))
+            if rc != 0:
+                _native.check(rc, "zmpc_rollout")
+        launch.hist, launch.status, launch.inputs = hist, status, keep
+        return launch
+
+    def rollout(self, zmax, zmin, x0, kick=None, kick_step=-1, hist=None, status=None):
+        """Batched Wieber rollout → hist [B,n,2,3] (device), status [B] (see _rollout_args)."""
+        hist, status, (args, _) = self._rollout_args(zmax, zmin, x0, kick, kick_step, hist,
+                                                     status)
+        with torch.cuda.device(self.device):
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+            rc = _native.load().zmpc_rollout(*args, ctypes.c_void_p(stream))
+        _native.check(rc, "zmpc_rollout")
+        return hist, status
+
+    def _rollout_args(self, zmax, zmin, x0, kick, kick_step, hist, status):
+        """Batched Wieber rollout → hist [B,n,2,3] (device), status [B].
+
+        zmax/zmin: [B,n,2] per-walk CoP bounds, or [n,2] one CoP shared by every walk;
+        x0: [B,2,3]; kick: [B] velocity impulse subtracted from y at step kick_step.
+        """
+        zmax = self._as_dev(zmax)
+        x0 = self._as_dev(x0)
+        if x0.dim() != 3 or x0.shape[1:] != (2, 3):
+            raise ValueError(f"x0 must be [B, 2, 3], got {tuple(x0.shape)}")
+        B = int(x0.shape[0])
+        if zmax.dim() == 2 and zmax.shape[1] == 2:
+            n = int(zmax.shape[0])
+            zmin = self._as_dev(zmin, (n, 2))
+            bstride = 0
+        elif zmax.dim() == 3 and zmax.shape[2] == 2 and zmax.shape[0] == B:
+            n = int(zmax.shape[1])
+            zmin = self._as_dev(zmin, (B, n, 2))
+            bstride = 2 * n
+        else:
+            raise ValueError(f"z_max must be [B, n, 2] or [n, 2], got {tuple(zmax.shape)}")
+        kick_t = None if kick is None else self._as_dev(kick, (B,))
+        if hist is None:
+            hist = torch.empty((B, n, 2, 3), dtype=torch.float64, device=self._dev())
+        elif tuple(hist.shape) != (B, n, 2, 3) or hist.dtype != torch.float64 or \
+                hist.device != self._dev() or not hist.is_contiguous():
+            raise ValueError("hist must be a contiguous float64 [B, n, 2, 3] tensor on the "
+                             "plan's device")
+        if status is None:
+            status = torch.empty(B, dtype=torch.int32, device=self._dev())
+        args = (self._h, B, n, _ptr(zmax), _ptr(zmin), bstride, _ptr(x0), _ptr(kick_t),
+                int(kick_step), _ptr(hist), _ptr(status))
+        return hist, status, (args, (zmax, zmin, x0, kick_t))
+
+
+def get_plan(config, device=None) -> Plan:
+    """Cached plan for an MPCConfig (keyed on every field the hot path reads)."""
+    dev = _device_index(getattr(config, "backend", "hip")) if device is None else int(device)
+    key = (dev, int(config.horizon), float(config.dt), float(config.h), float(config.g),
+           float(config.Q), float(config.R), bool(config.strict))
+    p = _PLAN_CACHE.get(key)
+    if p is None:
+        p = Plan(dev, key[1], key[2], key[3], key[4], key[5], key[6], key[7])
+        _PLAN_CACHE[key] = p
+    return p

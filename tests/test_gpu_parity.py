@@ -1,0 +1,295 @@
+"""Parity of the HIP path (through the C-ABI) with the oracle and the reference's golden vectors.
+
+Tolerances: north_star's bar is CoM/ZMP RMSE <= 1e-6 against the reference NumPy solve; the
+unconstrained path is held to 1e-9 here (the reference's own BLAS noise floor is ~7e-13), the
+strict path to 1e-6 against the exact KKT-certified oracle (parity with OSQP unpinned).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden, rmse
+from oracle import zmp_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+from mpc_bipedal.config import MPCConfig  # noqa: E402
+from mpc_bipedal.controllers import ZMPController  # noqa: E402
+from mpc_bipedal.solver import Plan, get_plan  # noqa: E402
+from mpc_bipedal import _native  # noqa: E402
+
+H, G, Q, R, M = 0.75, 9.81, 1.0, 1e-6, 40.0
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a HIP device")
+    _native.load()
+
+
+def plan(N, strict=False, Qv=Q, Rv=R, h=H, dt=None):
+    dt = 1.5 / N if dt is None else dt
+    return Plan(torch.cuda.current_device(), N, dt, h, G, Qv, Rv, strict)
+
+
+# --------------------------------------------------------------------------- plan
+
+
+@pytest.mark.parametrize("N", (1, 10, 32, 64, 150, 512))
+def test_plan_matrices(N):
+    p = plan(N, strict=(N <= 512))
+    dt = 1.5 / N
+    Px, Pu = O.prediction_matrices(N, dt, H, G)
+    assert np.array_equal(p.export(_native.EXPORT_P), Pu[:, 0])      # bit-exact vs reference
+    assert np.array_equal(p.export(_native.EXPORT_PX), Px)
+    Mref = Pu.T @ Pu + R / Q * np.eye(N)
+    Md = p.export(_native.EXPORT_M)
+    assert np.abs(Md - Mref).max() <= 1e-13 * np.abs(Mref).max()    # MFMA (N>=64) / FMA
+    k, kx = O.gain_row(N, dt, H, G, Q, R)
+    assert np.abs(p.export(_native.EXPORT_K) - k).max() <= 1e-9 * np.abs(k).max()
+    assert np.allclose(p.export(_native.EXPORT_KX), kx, rtol=1e-9, atol=0)
+    Gd = p.export(_native.EXPORT_G)
+    Hz, V, _, _ = O.strict_matrices(N, dt, H, G, Q, R)
+    Gref = np.linalg.inv(Hz)
+    assert np.abs(Gd - Gref).max() <= 1e-10 * np.abs(Gref).max()
+
+
+@pytest.mark.parametrize("N", (10, 64, 150, 512))
+def test_plan_gain_vs_reference_inverse(N):
+    d = golden(f"predict_n{N}.npz")
+    p = plan(N, dt=float(d["dt"]))
+    k = p.export(_native.EXPORT_K)
+    assert np.abs(k - d["gain_k"]).max() <= 1e-9 * np.abs(d["gain_k"]).max()
+    assert np.allclose(p.export(_native.EXPORT_KX), d["gain_kPx"], rtol=1e-9, atol=0)
+
+
+# --------------------------------------------------------------------------- drop-in API
+
+
+@pytest.mark.parametrize("N", (10, 64, 150, 512))
+def test_controller_com_trajectory_vs_reference(N):
+    d = golden(f"walk_n{N}.npz")
+    cfg = MPCConfig(horizon=N, strict=False, add_force=True)
+    c = ZMPController(cfg)
+    com, y_hist = c.generate_com_trajectory(np.zeros((3, 1)), np.zeros((3, 1)), d["zmax"],
+                                            d["zmin"])
+    assert com.shape == d["com_force"].shape and y_hist.shape == d["y_hist_force"].shape
+    assert rmse(com, d["com_force"]) <= 1e-9
+    zmp = np.tensordot(y_hist[:, :, 0], c.C, axes=([1], [0]))   # run_mpc.py:294
+    assert rmse(zmp, d["zmp_y_force"]) <= 1e-9
+    assert np.abs(y_hist - d["y_hist_force"]).max() <= 1e-7
+    xs, ys = c.generate_state_trajectory_wieber(np.zeros((3, 1)), np.zeros((3, 1)), d["zmax"],
+                                                d["zmin"])
+    assert np.abs(xs - d["state_x_hist"]).max() <= 1e-7
+    assert np.abs(ys - d["state_y_hist"]).max() <= 1e-7
+    if "com_noforce" in d:
+        c2 = ZMPController(MPCConfig(horizon=N, strict=False, add_force=False))
+        com2, _ = c2.generate_com_trajectory_wieber(np.zeros((3, 1)), np.zeros((3, 1)),
+                                                    d["zmax"], d["zmin"])
+        assert rmse(com2, d["com_noforce"]) <= 1e-9
+        xs, ys = c2.generate_state_trajectory_wieber(d["state_x0"], d["state_y0"], d["zmax"],
+                                                     d["zmin"])
+        assert np.abs(xs - d["state_x_hist_x0"]).max() <= 1e-7
+        assert np.abs(ys - d["state_y_hist_x0"]).max() <= 1e-7
+
+
+@pytest.mark.parametrize("N", (10, 64, 150, 512))
+def test_predict_wieber_axis_vs_reference(N):
+    d = golden(f"predict_n{N}.npz")
+    for c in range(len(d["x"])):
+        cfg = MPCConfig(horizon=N, strict=False, Q=float(d["Q"][c]), R=float(d["R"][c]),
+                        h=float(d["h"][c]), g=float(d["g"][c]))
+        out = ZMPController(cfg).predict_wieber_axis(d["x"][c], N, d["zmax"][c], d["zmin"][c])
+        ref = d["out"][c]
+        assert out.shape == (3, 1)
+        assert np.abs(out - ref).max() <= 1e-9 * max(1.0, np.abs(ref).max()), c
+
+
+def test_batched_step_vs_reference():
+    d = golden("predict_n150.npz")
+    p = plan(150, dt=float(d["dt"]))
+    out, st = p.step(d["x"][:64, :, 0], d["zmax"][:64, :, 0], d["zmin"][:64, :, 0])
+    assert np.abs(out.cpu().numpy() - d["out"][:64, :, 0]).max() <= 1e-9 * np.abs(d["out"]).max()
+    assert int(st.abs().max()) == 0
+
+
+# --------------------------------------------------------------------------- batches
+
+
+def synthetic_batch(B, N, seed=20251226, F_max=800.0):
+    """SURVEY §8d config-2 style batch: default CoP + rigid offsets, random x0 and F_ext."""
+    cop = golden(f"walk_n{N}.npz")
+    rng = np.random.default_rng(seed)
+    off = rng.uniform(-0.02, 0.02, (B, 1, 2))
+    zmax = cop["zmax"][None] + off
+    zmin = cop["zmin"][None] + off
+    x0 = np.zeros((B, 2, 3))
+    x0[:, :, 0] = rng.uniform(-0.01, 0.01, (B, 2))
+    F = rng.uniform(0.0, F_max, B)
+    return zmax, zmin, x0, F, float(cop["dt"])
+
+
+@pytest.mark.parametrize("N", (64, 150))
+def test_batch_unconstrained_vs_oracle(N):
+    zmax, zmin, x0, F, dt = synthetic_batch(256, N)
+    n = zmax.shape[1]
+    kick = dt * F / M
+    p = plan(N, dt=dt)
+    hist, st = p.rollout(zmax, zmin, x0, kick=kick, kick_step=n // 2)
+    ref = O.rollout_gain(zmax, zmin, x0, N, dt, H, G, Q, R, kick, n // 2)
+    h = hist.cpu().numpy()
+    assert np.abs(h - ref).max() <= 1e-8
+    assert rmse(h[..., 0], ref[..., 0]) <= 1e-10
+    assert int(st.abs().max()) == 0
+
+
+def test_shared_cop_equals_dense():
+    zmax, zmin, x0, F, dt = synthetic_batch(64, 150)
+    n = zmax.shape[1]
+    cop = golden("walk_n150.npz")
+    p = plan(150, dt=dt)
+    kick = dt * F / M
+    h_shared, _ = p.rollout(cop["zmax"], cop["zmin"], x0, kick=kick, kick_step=n // 2)
+    dense_x = np.repeat(cop["zmax"][None], 64, 0)
+    dense_n = np.repeat(cop["zmin"][None], 64, 0)
+    h_dense, _ = p.rollout(dense_x, dense_n, x0, kick=kick, kick_step=n // 2)
+    assert torch.equal(h_shared, h_dense)
+
+
+@pytest.mark.parametrize("n", (1, 2, 3, 65, 130, 513, 700))
+def test_walk_lengths(n):
+    """Ragged lengths: n=1 (no solve), chunk boundaries of the lane scan and of the
+    correlation passes."""
+    rng = np.random.default_rng(n)
+    N = 40
+    dt = 1.5 / N
+    ctr = np.cumsum(rng.normal(0, 0.01, (3, n, 2)), 1)
+    zmax, zmin = ctr + 0.05, ctr - 0.05
+    x0 = rng.normal(0, 0.01, (3, 2, 3))
+    kick = np.array([0.1, 0.0, -0.2])
+    p = plan(N, dt=dt)
+    hist, _ = p.rollout(zmax, zmin, x0, kick=kick, kick_step=n // 2)
+    ref = O.rollout_gain(zmax, zmin, x0, N, dt, H, G, Q, R, kick, n // 2)
+    assert np.abs(hist.cpu().numpy() - ref).max() <= 1e-8
+
+
+def test_kick_step_out_of_range_is_no_kick():
+    zmax, zmin, x0, F, dt = synthetic_batch(8, 64)
+    p = plan(64, dt=dt)
+    a, _ = p.rollout(zmax, zmin, x0, kick=np.full(8, 3.0), kick_step=10 ** 6)
+    b, _ = p.rollout(zmax, zmin, x0)
+    assert torch.equal(a, b)
+
+
+def test_empty_batch():
+    p = plan(64)
+    hist, st = p.rollout(np.zeros((0, 10, 2)), np.zeros((0, 10, 2)), np.zeros((0, 2, 3)))
+    assert hist.shape == (0, 10, 2, 3)
+
+
+def test_full_size_config2_properties():
+    """BASELINE config 2 size (B=4096, N=150): oracle on a sample + translation invariance
+    over the whole batch (x0 + δe0 and bounds + δ shift every position by δ exactly)."""
+    B = 4096
+    zmax, zmin, x0, F, dt = synthetic_batch(B, 150)
+    n = zmax.shape[1]
+    kick = dt * F / M
+    p = plan(150, dt=dt)
+    hist, st = p.rollout(zmax, zmin, x0, kick=kick, kick_step=n // 2)
+    assert int(st.abs().max()) == 0
+    idx = np.arange(0, B, 64)
+    ref = O.rollout_gain(zmax[idx], zmin[idx], x0[idx], 150, dt, H, G, Q, R, kick[idx], n // 2)
+    assert np.abs(hist.cpu().numpy()[idx] - ref).max() <= 1e-8
+    delta = 0.0625  # exactly representable: the shifted problem is exact in FP64
+    x1 = x0.copy()
+    x1[:, :, 0] += delta
+    h2, _ = p.rollout(zmax + delta, zmin + delta, x1, kick=kick, kick_step=n // 2)
+    diff = (h2 - hist).cpu().numpy()
+    assert np.abs(diff[..., 0] - delta).max() <= 1e-9
+    assert np.abs(diff[..., 1:]).max() <= 1e-7
+
+
+# --------------------------------------------------------------------------- strict
+
+
+@pytest.mark.parametrize("N", (16, 64, 150))
+def test_strict_step_vs_oracle(N):
+    d = golden("strict_oracle.npz")
+    p = plan(N, strict=True)
+    out, st = p.step(d[f"step{N}_x"], d[f"step{N}_zmax"], d[f"step{N}_zmin"])
+    ref = d[f"step{N}_out"]
+    assert int(st.abs().max()) == 0
+    assert np.abs(out.cpu().numpy() - ref).max() <= 1e-7 * max(1.0, np.abs(ref).max())
+
+
+@pytest.mark.parametrize("N", (64, 150))
+@pytest.mark.parametrize("F", (0, 400, 800))
+def test_strict_rollout_vs_oracle(N, F):
+    d = golden("strict_oracle.npz")
+    zx, zn = d[f"n{N}_zmax"], d[f"n{N}_zmin"]
+    n = len(zx)
+    dt = 1.5 / N
+    cfg = MPCConfig(horizon=N, strict=True, add_force=F > 0, F_ext=float(F))
+    c = ZMPController(cfg)
+    com, y_hist = c.generate_com_trajectory(np.zeros((3, 1)), np.zeros((3, 1)), zx, zn)
+    ref = d[f"n{N}_F{F}_hist"]
+    assert rmse(com, ref[:, :, 0]) <= 1e-6
+    assert rmse(com, ref[:, :, 0]) <= 1e-9 or F == 800
+    zmp = y_hist[:, :, 0] @ c.C
+    assert rmse(zmp, ref[:, 1, :] @ c.C) <= 1e-6
+    # the planned ZMP respects the bounds (strict semantics)
+    assert np.all(zmp[1:] <= zx[1:, 1] + 1e-9) and np.all(zmp[1:] >= zn[1:, 1] - 1e-9)
+
+
+@pytest.mark.parametrize("N", (64, 150))
+def test_strict_rollout_x0_vs_oracle(N):
+    d = golden("strict_oracle.npz")
+    c = ZMPController(MPCConfig(horizon=N, strict=True))
+    xs, ys = c.generate_state_trajectory_wieber(d[f"n{N}_x0"], d[f"n{N}_y0"], d[f"n{N}_zmax"],
+                                                d[f"n{N}_zmin"])
+    ref = d[f"n{N}_x0_hist"]
+    assert rmse(xs[:, 0, 0], ref[:, 0, 0]) <= 1e-9
+    assert rmse(ys[:, 0, 0], ref[:, 1, 0]) <= 1e-9
+
+
+def test_strict_equals_unconstrained_when_inactive():
+    zmax, zmin, x0, F, dt = synthetic_batch(32, 64, F_max=50.0)
+    n = zmax.shape[1]
+    zx, zn = zmax + 5.0, zmin - 5.0
+    kick = dt * F / M
+    hs, st = plan(64, strict=True, dt=dt).rollout(zx, zn, x0, kick=kick, kick_step=n // 2)
+    hu, _ = plan(64, dt=dt).rollout(zx, zn, x0, kick=kick, kick_step=n // 2)
+    assert int(st.abs().max()) == 0
+    assert np.abs((hs - hu).cpu().numpy()).max() <= 1e-8
+
+
+def test_strict_batch_vs_oracle_sample():
+    """Config-3 style batch (offsets, F_ext ~ U(0,800)): a sample of walks vs the oracle."""
+    B = 64
+    zmax, zmin, x0, F, dt = synthetic_batch(B, 150, seed=3)
+    n = zmax.shape[1]
+    kick = dt * F / M
+    hist, st = plan(150, strict=True, dt=dt).rollout(zmax, zmin, x0, kick=kick,
+                                                     kick_step=n // 2)
+    assert int(st.abs().max()) == 0
+    h = hist.cpu().numpy()
+    for b in (0, 7, 31, 63):
+        ref = O.rollout_strict(x0[b, 0], x0[b, 1], zmax[b], zmin[b], 150, dt, H, G, Q, R,
+                               kick=kick[b], kick_step=n // 2)
+        assert rmse(h[b, :, :, 0], ref[:, :, 0]) <= 1e-6, b
+
+
+def test_strict_translation_invariance_full_batch():
+    B = 2048
+    zmax, zmin, x0, F, dt = synthetic_batch(B, 150, seed=5)
+    n = zmax.shape[1]
+    kick = dt * F / M
+    p = plan(150, strict=True, dt=dt)
+    h1, s1 = p.rollout(zmax, zmin, x0, kick=kick, kick_step=n // 2)
+    x1 = x0.copy()
+    x1[:, :, 0] += 0.0625
+    h2, s2 = p.rollout(zmax + 0.0625, zmin + 0.0625, x1, kick=kick, kick_step=n // 2)
+    assert int(s1.abs().max()) == 0 and int(s2.abs().max()) == 0
+    d = (h2 - h1).cpu().numpy()
+    assert np.abs(d[..., 0] - 0.0625).max() <= 1e-7

@@ -1,0 +1,138 @@
+"""Host-side logic that needs no GPU: config, model, input producer, C-ABI symbol table,
+controller argument handling."""
+import ctypes
+import os
+import re
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, PKG, golden
+
+from mpc_bipedal.config import MPCConfig
+from mpc_bipedal.generators import CoPGenerator, generate_footsteps
+from mpc_bipedal.models.lipm_model import LIPMModel, lipm_matrices, prediction_matrices
+from mpc_bipedal import _native
+
+STATE_CODE = {"STANDING": 0, "DOUBLE_SUPPORT": 1, "SINGLE_SUPPORT": 2}
+
+
+def test_config_defaults_match_reference():
+    """Field defaults of config.py:13-87 and the dt rule of :84-87."""
+    c = MPCConfig()
+    assert c.horizon == 150 and c.dt == 1.5 / 150
+    assert (c.Q, c.R, c.S, c.h, c.g, c.m, c.F_ext) == (1.0, 1e-6, 1.0, 0.75, 9.81, 40.0, 400.0)
+    assert c.strict is True and c.add_force is True and c.method == "wieber"
+    assert (c.ssp_duration, c.dsp_duration, c.standing_duration) == (0.24, 0.01, 0.5)
+    assert (c.distance, c.step_length, c.foot_spread) == (2.1, 0.3, 0.1)
+    assert len(c.left_foot_polytope) == 11 and len(c.right_foot_polytope) == 11
+    assert MPCConfig(horizon=64).dt == 1.5 / 64
+    assert MPCConfig(dt=0.02).dt == 0.02
+
+
+@pytest.mark.parametrize("tag", ["default_n150", "default_n10", "default_n64", "default_n512",
+                                 "classdefaults_n150", "long_n100", "short_n200"])
+def test_cop_generator_bit_exact(tag):
+    d = golden(f"cop_{tag}.npz")
+    cfg = MPCConfig(horizon=int(d["horizon"]), dt=float(d["dt"]), distance=float(d["distance"]),
+                    step_length=float(d["step_length"]), foot_spread=float(d["foot_spread"]),
+                    ssp_duration=float(d["ssp_duration"]), dsp_duration=float(d["dsp_duration"]),
+                    standing_duration=float(d["standing_duration"]))
+    zx, zn, st = CoPGenerator(cfg).generate_cop_trajectory()
+    assert np.array_equal(zx, d["zmax"]) and np.array_equal(zn, d["zmin"])
+    assert np.array_equal(np.array([STATE_CODE[s.value] for s in st]), d["states"])
+
+
+def test_footsteps():
+    f = generate_footsteps(2.1, 0.3, 0.1)
+    assert len(f) == 10
+    assert f[0].y == -0.1 and f[1].y == 0.1 and f[-1].x == f[-2].x
+    assert np.isclose(f[2].z_max[0] - f[2].z_min[0], 0.11)
+
+
+@pytest.mark.parametrize("N", (10, 64, 150, 512))
+def test_model_prediction_matrices_bit_exact(N):
+    d = golden(f"predict_n{N}.npz")
+    Px, Pu = prediction_matrices(N, float(d["dt"]), 0.75, 9.81)
+    assert np.array_equal(Px, d["Px"]) and np.array_equal(Pu[:, 0], d["Pu_col0"])
+
+
+def test_lipm_model():
+    cfg = MPCConfig()
+    m = LIPMModel(cfg)
+    A, B, C = lipm_matrices(cfg.dt, cfg.h, cfg.g)
+    assert m.get_state_dimension() == 3
+    x = np.array([[0.1], [0.2], [0.3]])
+    assert np.array_equal(m.step(x, 2.0), A @ x + B * 2.0)
+    assert np.allclose(m.get_zmp(x[:, 0]), 0.1 - 0.75 / 9.81 * 0.3)
+
+
+def _header_symbols():
+    src = open(os.path.join(ROOT, "include", "zmpc.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(zmpc_[a-z_]+)\s*\(", src)))
+
+
+def test_header_and_binding_agree():
+    syms = _header_symbols()
+    assert set(syms) == set(_native.SIGNATURES), syms
+
+
+def test_library_loads_and_exports_every_symbol():
+    """The C-ABI library loads without a GPU and exports every declared entry point."""
+    if not os.path.exists(_native.LIB_PATH):
+        pytest.skip("libzmpc.so not built (run __graft_entry__.build())")
+    lib = ctypes.CDLL(_native.LIB_PATH)
+    for s in _header_symbols():
+        assert hasattr(lib, s), s
+    out = subprocess.run(["nm", "-D", "--defined-only", _native.LIB_PATH], capture_output=True,
+                         text=True).stdout
+    exported = set(re.findall(r" T (zmpc_\w+)", out))
+    assert set(_header_symbols()) <= exported
+    lib = _native.load()
+    assert lib.zmpc_abi_version() == 1
+    assert lib.zmpc_last_error() == b""
+
+
+def test_argument_errors_without_gpu():
+    """Argument validation happens before any device call and reports through last_error."""
+    if not os.path.exists(_native.LIB_PATH):
+        pytest.skip("libzmpc.so not built")
+    lib = _native.load()
+    h = ctypes.c_void_p()
+    rc = lib.zmpc_plan_create(0, 0, 0.01, 5e-5, 1.6e-7, 0.07, 7e-4, 1.0, 1e-6, 0, None,
+                              ctypes.byref(h))
+    assert rc == _native.ZMPC_EINVAL and b"horizon" in lib.zmpc_last_error()
+    rc = lib.zmpc_rollout(None, 1, 10, None, None, 20, None, None, -1, None, None, None)
+    assert rc == _native.ZMPC_EINVAL
+    rc = lib.zmpc_step(None, 1, None, None, None, None, None, None)
+    assert rc == _native.ZMPC_EINVAL
+
+
+def test_router_errors():
+    from mpc_bipedal.controllers import ZMPController
+    c = ZMPController(MPCConfig())
+    with pytest.raises(ValueError, match="z_max and z_min are required"):
+        c.generate_com_trajectory(np.zeros((3, 1)), np.zeros((3, 1)))
+    c2 = ZMPController(MPCConfig(method="herdt"))
+    with pytest.raises(ValueError, match="v_ref and state_ref"):
+        c2.generate_com_trajectory(np.zeros((3, 1)), np.zeros((3, 1)))
+    with pytest.raises(NotImplementedError):
+        c2.generate_com_trajectory(np.zeros((3, 1)), np.zeros((3, 1)), v_ref=np.zeros(3),
+                                   state_ref=[])
+    c3 = ZMPController(MPCConfig(method="foo"))
+    with pytest.raises(ValueError, match="Unknown method"):
+        c3.generate_com_trajectory(np.zeros((3, 1)), np.zeros((3, 1)))
+    assert np.array_equal(c.C, np.array([1.0, 0.0, -0.75 / 9.81]))
+
+
+def test_product_has_no_oracle_or_cpu_solver_import():
+    """The product package never imports the oracle (test infrastructure only)."""
+    for dirpath, _, files in os.walk(os.path.join(PKG, "mpc_bipedal")):
+        for f in files:
+            if f.endswith(".py"):
+                src = open(os.path.join(dirpath, f)).read()
+                assert "oracle" not in src.replace("no oracle", ""), f
+                assert "linalg.inv" not in src and "linalg.solve" not in src, f
