@@ -19,6 +19,8 @@
 //   3. chunked affine scan over the 64 lanes with P = Ā^C (Ā = A - B kxᵀ), Kogge-Stone;
 //   4. each lane replays its chunk in the reference form x⁺ = A x + B u, applies the
 //      F_ext kick (:105-106) and stores the states.
+#include <cstdlib>
+
 #include "zmpc_internal.h"
 
 namespace {
@@ -68,7 +70,7 @@ __global__ void __launch_bounds__(64) zmpc_rollout_unc_kernel(
     int Kpad, int n, LipmConsts lc, const double* __restrict__ k, const double* __restrict__ kxp,
     const double* __restrict__ zmax, const double* __restrict__ zmin, int64_t bstride,
     const double* __restrict__ x0, const double* __restrict__ kick, int64_t kick_step,
-    double* __restrict__ hist, int32_t* __restrict__ status) {
+    double* __restrict__ hist, int32_t* __restrict__ status, int dbg) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int64_t b = blockIdx.x;
   const int lane = threadIdx.x;
@@ -84,7 +86,7 @@ __global__ void __launch_bounds__(64) zmpc_rollout_unc_kernel(
   // ---- 1. z_ref for both axes, padded with the last row -------------------------------
   const double* zmx = zmax + b * bstride;
   const double* zmn = zmin + b * bstride;
-  for (int e = lane; e < 2 * n; e += 64) {
+  for (int e = lane; e < ((dbg & 8) ? 0 : 2 * n); e += 64) {
     const double zr = (zmx[e] + zmn[e]) / 2;  // z_ref = (z_max + z_min) / 2
     if (e & 1)
       zr1[e >> 1] = zr;
@@ -102,7 +104,7 @@ __global__ void __launch_bounds__(64) zmpc_rollout_unc_kernel(
   __syncthreads();
 
   // ---- 2. f_i = Σ_j k_j z_ref[i+1+j], 8 outputs per lane, sliding register window -----
-  for (int pass = 0; pass < passes; ++pass) {
+  for (int pass = 0; pass < ((dbg & 1) ? 0 : passes); ++pass) {
     const int i0 = pass * 64 * kCW + lane * kCW;
     double a0[kCW], a1[kCW], w0[kCW], w1[kCW];
 #pragma unroll
@@ -179,7 +181,7 @@ __global__ void __launch_bounds__(64) zmpc_rollout_unc_kernel(
   }
   // inclusive Kogge-Stone: T_l += P^d T_{l-d}
   Mat3 Pd = P;
-  for (int d = 1; d < 64; d <<= 1) {
+  for (int d = 1; d < ((dbg & 2) ? 1 : 64); d <<= 1) {
     double u0[3], u1[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -219,6 +221,7 @@ __global__ void __launch_bounds__(64) zmpc_rollout_unc_kernel(
     lipm_step(lc, y, uy, yn);
     if (m == kick_step) yn[1] -= kk;
     double* o = hb + (int64_t)(m + 1) * 6;
+    if (dbg & 4) continue;
     reinterpret_cast<double2*>(o)[0] = make_double2(xn[0], xn[1]);
     reinterpret_cast<double2*>(o)[1] = make_double2(xn[2], yn[0]);
     reinterpret_cast<double2*>(o)[2] = make_double2(yn[1], yn[2]);
@@ -282,9 +285,13 @@ hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, con
     if (status) return hipMemsetAsync(status, 0, sizeof(int32_t) * B, s);
     return hipSuccess;
   }
+  static const int dbg = [] {
+    const char* e = getenv("ZMPC_DEBUG_ROLLOUT");  // diagnostic ablation bits (0 in production)
+    return e ? atoi(e) : 0;
+  }();
   hipLaunchKernelGGL(zmpc_rollout_unc_kernel, dim3((unsigned)B), dim3(64), lds, s, p->Kpad,
                      (int)n, p->lc, p->k, p->kx, zmax, zmin, bstride, x0, kick, kick_step, hist,
-                     status);
+                     status, dbg);
   return hipGetLastError();
 }
 

@@ -1,0 +1,37 @@
+"""Diagnostic: time the unconstrained rollout kernel per phase (ZMPC_DEBUG_ROLLOUT bits:
+1 skip correlation, 2 skip lane scan, 4 skip history stores, 8 skip bound loads) and batch.
+Each configuration runs in a child process (the env var is read once per process)."""
+import json
+import os
+import subprocess
+import sys
+
+CHILD = r'''
+import sys, os, json, numpy as np, torch
+sys.path.insert(0, os.environ["PKG"])
+from mpc_bipedal.solver import Plan
+B = int(sys.argv[1]); N = int(sys.argv[2]); n = int(sys.argv[3])
+p = Plan(0, N, 1.5 / N, 0.75, 9.81, 1.0, 1e-6, False)
+rng = np.random.default_rng(0)
+zc = np.cumsum(rng.normal(0, 0.01, (B, n, 2)), 1)
+zmax = torch.as_tensor(zc + 0.05, device="cuda"); zmin = torch.as_tensor(zc - 0.05, device="cuda")
+x0 = torch.zeros((B, 2, 3), dtype=torch.float64, device="cuda")
+L = p.rollout_launcher(zmax, zmin, x0)
+for _ in range(3): L()
+torch.cuda.synchronize()
+ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
+for a, b in ev:
+    a.record(); L(); b.record()
+torch.cuda.synchronize()
+print(json.dumps(dict(B=B, N=N, n=n, dbg=os.environ.get("ZMPC_DEBUG_ROLLOUT", "0"),
+                      us=float(np.median([a.elapsed_time(b) for a, b in ev])) * 1e3)))
+'''
+
+root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+env0 = dict(os.environ, PKG=os.path.join(root, "model-predictive-control-for-bipedal-locomotion_amd"))
+for B, N, n in [(1024, 150, 420), (4096, 150, 420), (16384, 150, 420)]:
+    for dbg in (0, 1, 2, 4, 8, 15):
+        env = dict(env0, ZMPC_DEBUG_ROLLOUT=str(dbg))
+        r = subprocess.run([sys.executable, "-c", CHILD, str(B), str(N), str(n)], env=env,
+                           capture_output=True, text=True, timeout=120)
+        print(r.stdout.strip() or r.stderr[-500:], flush=True)

@@ -22,7 +22,7 @@ timeout -k 10 600 python bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
 rc=$?; echo "bench rc=$rc"; cat "$OUT/bench.json"; tail -3 "$OUT/bench.err"
 if [ $rc -ne 0 ]; then exit $rc; fi
 
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o bench -- \
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- \
     python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
 rc=$?; echo "rocprof rc=$rc"
 find "$OUT/prof" -name "*stats*" | head -5
