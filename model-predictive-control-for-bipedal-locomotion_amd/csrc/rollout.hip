@@ -19,13 +19,13 @@
 //   3. chunked affine scan over the 64 lanes with P = Ā^C (Ā = A - B kxᵀ), Kogge-Stone;
 //   4. each lane replays its chunk in the reference form x⁺ = A x + B u, applies the
 //      F_ext kick (:105-106) and stores the states.
+#include <climits>
+#include <cstdint>
 #include <cstdlib>
 
 #include "zmpc_internal.h"
 
 namespace {
-
-constexpr int kCW = 8;  // outputs per lane in the correlation register tile
 
 struct Mat3 {
   double m[9];
@@ -58,84 +58,137 @@ __device__ __forceinline__ void lipm_step(const LipmConsts& c, const double* x, 
 
 }  // namespace
 
-size_t zmpc_rollout_unc_lds_bytes(int Kpad, int64_t n) {
-  const int64_t nsteps = n - 1;
-  const int64_t passes = (nsteps + 64 * kCW - 1) / (64 * kCW);
-  const int64_t Lz = passes * 64 * kCW + Kpad + 1;
-  const int64_t nf = ((nsteps + 1) + 1) & ~1LL;
-  return (size_t)(2 * Lz + 2 * nf) * sizeof(double);
+// Correlation tile width: outputs per lane per pass, chosen per walk length so that
+// passes·64·CW barely covers the n−1 timesteps (n = 420 → CW = 7: 448 outputs, 1 pass).
+static int pick_cw(int64_t nsteps) {
+  int best = 8;
+  int64_t best_cost = INT64_MAX;
+  for (int cw = 8; cw >= 1; --cw) {
+    const int64_t cost = ((nsteps + 64 * cw - 1) / (64 * cw)) * cw;
+    if (cost < best_cost) {
+      best_cost = cost;
+      best = cw;
+    }
+  }
+  return best;
 }
 
+// LDS layout of z_ref: lane l's chunk starts at t = l·CW; for even CW one pad double per CW
+// keeps the 64 lanes' ds_read_b64 on distinct banks (lane stride CW+1 doubles, odd).
+template <int CW>
+struct ZrLayout {
+  static constexpr int kPad = (CW % 2 == 0) ? 1 : 0;
+  __host__ __device__ static constexpr int idx(int t) { return t + kPad * (t / CW); }
+};
+
+struct RolloutGeom {
+  int cw, passes, kc, lz, lzp, nf;
+};
+
+static RolloutGeom rollout_geom(int N, int64_t n) {
+  RolloutGeom g;
+  const int64_t nsteps = n - 1;
+  g.cw = pick_cw(nsteps);
+  g.passes = (int)((nsteps + 64 * g.cw - 1) / (64 * g.cw));
+  g.kc = (N + g.cw - 1) / g.cw * g.cw;           // k loop bound (k zero-padded)
+  g.lz = g.passes * 64 * g.cw + g.kc + 1;         // z_ref samples staged (padded with last)
+  const int pad = (g.cw % 2 == 0) ? 1 : 0;
+  g.lzp = g.lz + pad * (g.lz / g.cw) + 1;         // LDS doubles per axis
+  g.lzp = (g.lzp + 1) & ~1;
+  g.nf = g.passes == 1 ? 0 : (int)((nsteps + 2) & ~1LL);   // f lives in LDS only if passes > 1
+  return g;
+}
+
+size_t zmpc_rollout_unc_lds_bytes(int N, int64_t n) {
+  const RolloutGeom g = rollout_geom(N, n);
+  return (size_t)(2 * g.lzp + 2 * g.nf) * sizeof(double);
+}
+
+// One wave per walk.  REGF (n − 1 <= 64·CW, a single correlation pass): lane l's CW
+// correlation outputs are exactly its scan chunk [l·CW, l·CW + CW), so f never leaves
+// registers; otherwise f goes through LDS and the scan chunk is ⌈(n−1)/64⌉.
+template <int CW, bool REGF>
 __global__ void __launch_bounds__(64) zmpc_rollout_unc_kernel(
-    int Kpad, int n, LipmConsts lc, const double* __restrict__ k, const double* __restrict__ kxp,
-    const double* __restrict__ zmax, const double* __restrict__ zmin, int64_t bstride,
-    const double* __restrict__ x0, const double* __restrict__ kick, int64_t kick_step,
-    double* __restrict__ hist, int32_t* __restrict__ status, int dbg) {
+    int kc, int lz, int lzp, int n, LipmConsts lc, const double* __restrict__ k,
+    const double* __restrict__ kxp, const double* __restrict__ zmax,
+    const double* __restrict__ zmin, int64_t bstride, const double* __restrict__ x0,
+    const double* __restrict__ kick, int64_t kick_step, double* __restrict__ hist,
+    int32_t* __restrict__ status, int dbg) {
+  using ZL = ZrLayout<CW>;
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int64_t b = blockIdx.x;
   const int lane = threadIdx.x;
   const int nsteps = n - 1;
-  const int passes = (nsteps + 64 * kCW - 1) / (64 * kCW);
-  const int Lz = passes * 64 * kCW + Kpad + 1;
-  const int nf = (nsteps + 2) & ~1;
+  const int passes = REGF ? 1 : (nsteps + 64 * CW - 1) / (64 * CW);
   double* zr0 = smem;
-  double* zr1 = smem + Lz;
-  double* f0 = smem + 2 * Lz;
-  double* f1 = f0 + nf;
+  double* zr1 = smem + lzp;
+  double* f0 = smem + 2 * lzp;                 // LDS f (REGF == false only)
+  double* f1 = f0 + ((nsteps + 2) & ~1);
 
   // ---- 1. z_ref for both axes, padded with the last row -------------------------------
-  const double* zmx = zmax + b * bstride;
-  const double* zmn = zmin + b * bstride;
-  for (int e = lane; e < ((dbg & 8) ? 0 : 2 * n); e += 64) {
-    const double zr = (zmx[e] + zmn[e]) / 2;  // z_ref = (z_max + z_min) / 2
-    if (e & 1)
-      zr1[e >> 1] = zr;
-    else
-      zr0[e >> 1] = zr;
+  // one 16-B (x, y) sample per lane from each bound array: coalesced 1 KiB per instruction
+  const double2* zmx = reinterpret_cast<const double2*>(zmax + b * bstride);
+  const double2* zmn = reinterpret_cast<const double2*>(zmin + b * bstride);
+  for (int t = lane; t < ((dbg & 8) ? 0 : n); t += 64) {
+    const double2 hi = zmx[t], lo = zmn[t];
+    zr0[ZL::idx(t)] = (hi.x + lo.x) / 2;  // z_ref = (z_max + z_min) / 2
+    zr1[ZL::idx(t)] = (hi.y + lo.y) / 2;
   }
   {
-    const double last0 = (zmx[2 * n - 2] + zmn[2 * n - 2]) / 2;
-    const double last1 = (zmx[2 * n - 1] + zmn[2 * n - 1]) / 2;
-    for (int t = n + lane; t < Lz; t += 64) {
-      zr0[t] = last0;
-      zr1[t] = last1;
+    const double2 hi = zmx[n - 1], lo = zmn[n - 1];
+    const double last0 = (hi.x + lo.x) / 2, last1 = (hi.y + lo.y) / 2;
+    for (int t = n + lane; t < lz; t += 64) {
+      zr0[ZL::idx(t)] = last0;
+      zr1[ZL::idx(t)] = last1;
     }
   }
   __syncthreads();
 
-  // ---- 2. f_i = Σ_j k_j z_ref[i+1+j], 8 outputs per lane, sliding register window -----
+  // ---- 2. f_i = Σ_j k_j z_ref[i+1+j], CW outputs per lane, sliding register window ----
+  double a0[CW], a1[CW];
   for (int pass = 0; pass < ((dbg & 1) ? 0 : passes); ++pass) {
-    const int i0 = pass * 64 * kCW + lane * kCW;
-    double a0[kCW], a1[kCW], w0[kCW], w1[kCW];
+    const int i0 = pass * 64 * CW + lane * CW;
+    // i0 is a multiple of CW, so idx(i0 + c) = idx(i0) + idx(c): compile-time offsets
+    const double* z0 = zr0 + ZL::idx(i0);
+    const double* z1 = zr1 + ZL::idx(i0);
+    double w0[CW], w1[CW];
 #pragma unroll
-    for (int m = 0; m < kCW; ++m) {
+    for (int m = 0; m < CW; ++m) {
       a0[m] = 0.0;
       a1[m] = 0.0;
-      w0[m] = zr0[i0 + 1 + m];
-      w1[m] = zr1[i0 + 1 + m];
+      w0[m] = z0[ZL::idx(1 + m)];
+      w1[m] = z1[ZL::idx(1 + m)];
     }
-    for (int j = 0; j < Kpad; j += kCW) {
+    for (int j = 0; j < kc; j += CW) {
 #pragma unroll
-      for (int jj = 0; jj < kCW; ++jj) {
+      for (int jj = 0; jj < CW; ++jj) {
         const double kj = k[j + jj];
 #pragma unroll
-        for (int m = 0; m < kCW; ++m) {
-          a0[m] = fma(kj, w0[(jj + m) % kCW], a0[m]);
-          a1[m] = fma(kj, w1[(jj + m) % kCW], a1[m]);
+        for (int m = 0; m < CW; ++m) {
+          a0[m] = fma(kj, w0[(jj + m) % CW], a0[m]);
+          a1[m] = fma(kj, w1[(jj + m) % CW], a1[m]);
         }
-        w0[jj] = zr0[i0 + 1 + j + jj + kCW];
-        w1[jj] = zr1[i0 + 1 + j + jj + kCW];
+        w0[jj] = z0[ZL::idx(1 + jj + CW)];
+        w1[jj] = z1[ZL::idx(1 + jj + CW)];
       }
+      z0 += CW + ZL::kPad;
+      z1 += CW + ZL::kPad;
     }
+    if constexpr (!REGF) {
 #pragma unroll
-    for (int m = 0; m < kCW; ++m) {
-      if (i0 + m < nsteps) {
-        f0[i0 + m] = a0[m];
-        f1[i0 + m] = a1[m];
+      for (int m = 0; m < CW; ++m) {
+        if (i0 + m < nsteps) {
+          f0[i0 + m] = a0[m];
+          f1[i0 + m] = a1[m];
+        }
       }
     }
   }
-  __syncthreads();
+  if (dbg & 1) {
+#pragma unroll
+    for (int m = 0; m < CW; ++m) a0[m] = a1[m] = 0.0;
+  }
+  if constexpr (!REGF) __syncthreads();
 
   // ---- 3. affine scan of x_{i+1} = Ā x_i + B f_i (+ kick) over 64 lane chunks ----------
   const double kx0 = kxp[0], kx1 = kxp[1], kx2 = kxp[2];
@@ -149,23 +202,29 @@ __global__ void __launch_bounds__(64) zmpc_rollout_unc_kernel(
 #pragma unroll
       for (int j = 0; j < 3; ++j) Ab.m[3 * i + j] = A[3 * i + j] - Bv[i] * kx[j];
   }
-  const int C = (nsteps + 63) / 64;  // steps per lane chunk
+  const int C = REGF ? CW : (nsteps + 63) / 64;  // steps per lane chunk
   const int mbeg = lane * C;
-  const int mend = min(mbeg + C, nsteps);
   const double kk = (kick != nullptr) ? kick[b] : 0.0;
 
   double s0[3] = {0.0, 0.0, 0.0}, s1[3] = {0.0, 0.0, 0.0};
-  for (int m = mbeg; m < mend; ++m) {
+  auto scan_step = [&](int m, double fx, double fy) {
     double t[3];
     matvec3(Ab, s0, t);
-    s0[0] = fma(Bv[0], f0[m], t[0]);
-    s0[1] = fma(Bv[1], f0[m], t[1]);
-    s0[2] = fma(Bv[2], f0[m], t[2]);
+    s0[0] = fma(Bv[0], fx, t[0]);
+    s0[1] = fma(Bv[1], fx, t[1]);
+    s0[2] = fma(Bv[2], fx, t[2]);
     matvec3(Ab, s1, t);
-    s1[0] = fma(Bv[0], f1[m], t[0]);
-    s1[1] = fma(Bv[1], f1[m], t[1]);
-    s1[2] = fma(Bv[2], f1[m], t[2]);
+    s1[0] = fma(Bv[0], fy, t[0]);
+    s1[1] = fma(Bv[1], fy, t[1]);
+    s1[2] = fma(Bv[2], fy, t[2]);
     if (m == kick_step) s1[1] -= kk;
+  };
+  if constexpr (REGF) {
+#pragma unroll
+    for (int q = 0; q < CW; ++q)
+      if (mbeg + q < nsteps) scan_step(mbeg + q, a0[q], a1[q]);
+  } else {
+    for (int m = mbeg; m < min(mbeg + C, nsteps); ++m) scan_step(m, f0[m], f1[m]);
   }
   Mat3 P = Ab;  // P = Ā^C
   for (int q = 1; q < C; ++q) P = matmul3(P, Ab);
@@ -206,34 +265,42 @@ __global__ void __launch_bounds__(64) zmpc_rollout_unc_kernel(
     y[i] = (lane == 0) ? xi1[i] : p1;
   }
 
-  // ---- 4. replay in the reference form and store ------------------------------------
+  // ---- 4. replay in the reference form x⁺ = A x + B u and store ---------------------
   double* hb = hist + b * (int64_t)n * 6;
   if (lane == 0) {
-    hb[0] = xi0[0]; hb[1] = xi0[1]; hb[2] = xi0[2];
-    hb[3] = xi1[0]; hb[4] = xi1[1]; hb[5] = xi1[2];
+    reinterpret_cast<double2*>(hb)[0] = make_double2(xi0[0], xi0[1]);
+    reinterpret_cast<double2*>(hb)[1] = make_double2(xi0[2], xi1[0]);
+    reinterpret_cast<double2*>(hb)[2] = make_double2(xi1[1], xi1[2]);
   }
-  bool finite = true;
-  for (int m = mbeg; m < mend; ++m) {
-    const double ux = f0[m] - (kx0 * x[0] + kx1 * x[1] + kx2 * x[2]);
-    const double uy = f1[m] - (kx0 * y[0] + kx1 * y[1] + kx2 * y[2]);
+  auto replay_step = [&](int m, double fx, double fy) {
+    const double ux = fx - (kx0 * x[0] + kx1 * x[1] + kx2 * x[2]);
+    const double uy = fy - (kx0 * y[0] + kx1 * y[1] + kx2 * y[2]);
     double xn[3], yn[3];
     lipm_step(lc, x, ux, xn);
     lipm_step(lc, y, uy, yn);
     if (m == kick_step) yn[1] -= kk;
-    double* o = hb + (int64_t)(m + 1) * 6;
-    if (dbg & 4) continue;
-    reinterpret_cast<double2*>(o)[0] = make_double2(xn[0], xn[1]);
-    reinterpret_cast<double2*>(o)[1] = make_double2(xn[2], yn[0]);
-    reinterpret_cast<double2*>(o)[2] = make_double2(yn[1], yn[2]);
+    if (!(dbg & 4)) {
+      double2* o = reinterpret_cast<double2*>(hb + (int64_t)(m + 1) * 6);
+      o[0] = make_double2(xn[0], xn[1]);
+      o[1] = make_double2(xn[2], yn[0]);
+      o[2] = make_double2(yn[1], yn[2]);
+    }
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
       x[i] = xn[i];
       y[i] = yn[i];
     }
+  };
+  if constexpr (REGF) {
+#pragma unroll
+    for (int q = 0; q < CW; ++q)
+      if (mbeg + q < nsteps) replay_step(mbeg + q, a0[q], a1[q]);
+  } else {
+    for (int m = mbeg; m < min(mbeg + C, nsteps); ++m) replay_step(m, f0[m], f1[m]);
   }
   if (status != nullptr) {
-    finite = isfinite(x[0]) && isfinite(x[1]) && isfinite(x[2]) && isfinite(y[0]) &&
-             isfinite(y[1]) && isfinite(y[2]);
+    const bool finite = isfinite(x[0]) && isfinite(x[1]) && isfinite(x[2]) &&
+                        isfinite(y[0]) && isfinite(y[1]) && isfinite(y[2]);
     const unsigned long long bad = __ballot(!finite);
     if (lane == 0) status[b] = bad ? ZMPC_ST_NONFINITE : 0;
   }
@@ -267,16 +334,25 @@ __global__ void __launch_bounds__(256) zmpc_step_unc_kernel(
   }
 }
 
+template <int CW>
+static void launch_unc(const RolloutGeom& g, size_t lds, hipStream_t s, int64_t B, int64_t n,
+                       const zmpc_plan* p, const double* zmax, const double* zmin,
+                       int64_t bstride, const double* x0, const double* kick, int64_t kick_step,
+                       double* hist, int32_t* status, int dbg) {
+  if (g.passes == 1)
+    hipLaunchKernelGGL((zmpc_rollout_unc_kernel<CW, true>), dim3((unsigned)B), dim3(64), lds, s,
+                       g.kc, g.lz, g.lzp, (int)n, p->lc, p->k, p->kx, zmax, zmin, bstride, x0,
+                       kick, kick_step, hist, status, dbg);
+  else
+    hipLaunchKernelGGL((zmpc_rollout_unc_kernel<CW, false>), dim3((unsigned)B), dim3(64), lds,
+                       s, g.kc, g.lz, g.lzp, (int)n, p->lc, p->k, p->kx, zmax, zmin, bstride,
+                       x0, kick, kick_step, hist, status, dbg);
+}
+
 hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, const double* zmax,
                                    const double* zmin, int64_t bstride, const double* x0,
-                                   const double* kick,
-                                   int64_t kick_step, double* hist, int32_t* status,
-                                   hipStream_t s, std::string* why) {
-  const size_t lds = zmpc_rollout_unc_lds_bytes(p->Kpad, n);
-  if (lds > 160 * 1024) {
-    *why = "walk too long for the LDS-resident rollout (n=" + std::to_string(n) + ")";
-    return hipErrorInvalidValue;
-  }
+                                   const double* kick, int64_t kick_step, double* hist,
+                                   int32_t* status, hipStream_t s, std::string* why) {
   if (n == 1) {
     // no QP solve: the history is the initial state only
     hipError_t e = hipMemcpyAsync(hist, x0, 6 * sizeof(double) * (size_t)B,
@@ -285,13 +361,27 @@ hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, con
     if (status) return hipMemsetAsync(status, 0, sizeof(int32_t) * B, s);
     return hipSuccess;
   }
+  const RolloutGeom g = rollout_geom(p->N, n);
+  const size_t lds = (size_t)(2 * g.lzp + 2 * g.nf) * sizeof(double);
+  if (lds > 160 * 1024) {
+    *why = "walk too long for the LDS-resident rollout (n=" + std::to_string(n) + ")";
+    return hipErrorInvalidValue;
+  }
   static const int dbg = [] {
     const char* e = getenv("ZMPC_DEBUG_ROLLOUT");  // diagnostic ablation bits (0 in production)
     return e ? atoi(e) : 0;
   }();
-  hipLaunchKernelGGL(zmpc_rollout_unc_kernel, dim3((unsigned)B), dim3(64), lds, s, p->Kpad,
-                     (int)n, p->lc, p->k, p->kx, zmax, zmin, bstride, x0, kick, kick_step, hist,
-                     status, dbg);
+  switch (g.cw) {
+#define ZMPC_CW(C)                                                                          \
+  case C:                                                                                   \
+    launch_unc<C>(g, lds, s, B, n, p, zmax, zmin, bstride, x0, kick, kick_step, hist, status, \
+                  dbg);                                                                     \
+    break;
+    ZMPC_CW(1) ZMPC_CW(2) ZMPC_CW(3) ZMPC_CW(4) ZMPC_CW(5) ZMPC_CW(6) ZMPC_CW(7) ZMPC_CW(8)
+#undef ZMPC_CW
+    default:
+      return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 
@@ -305,6 +395,16 @@ hipError_t zmpc_launch_step_unc(const zmpc_plan* p, int64_t B, const double* x,
 
 // The dynamic-LDS ceiling must be raised once per device for > 64 KiB requests.
 hipError_t zmpc_rollout_unc_set_attrs() {
-  return hipFuncSetAttribute((const void*)zmpc_rollout_unc_kernel,
-                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hipError_t e = hipSuccess;
+#define ZMPC_ATTR(C)                                                                        \
+  if (e == hipSuccess)                                                                      \
+    e = hipFuncSetAttribute((const void*)zmpc_rollout_unc_kernel<C, true>,                 \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);       \
+  if (e == hipSuccess)                                                                      \
+    e = hipFuncSetAttribute((const void*)zmpc_rollout_unc_kernel<C, false>,                \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  ZMPC_ATTR(1) ZMPC_ATTR(2) ZMPC_ATTR(3) ZMPC_ATTR(4) ZMPC_ATTR(5) ZMPC_ATTR(6) ZMPC_ATTR(7)
+  ZMPC_ATTR(8)
+#undef ZMPC_ATTR
+  return e;
 }
