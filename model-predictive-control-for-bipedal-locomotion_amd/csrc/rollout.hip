@@ -94,6 +94,9 @@ static RolloutGeom rollout_geom(int N, int64_t n) {
   g.lz = g.passes * 64 * g.cw + g.kc + 1;         // z_ref samples staged (padded with last)
   const int pad = (g.cw % 2 == 0) ? 1 : 0;
   g.lzp = g.lz + pad * (g.lz / g.cw) + 1;         // LDS doubles per axis
+  // the z_ref area doubles as the history staging buffer: at least half a walk of rows
+  const int64_t stage_min = ((n + 1) / 2 * 6 + 1) / 2;
+  if (g.lzp < stage_min) g.lzp = (int)stage_min;
   g.lzp = (g.lzp + 1) & ~1;
   g.nf = g.passes == 1 ? 0 : (int)((nsteps + 2) & ~1LL);   // f lives in LDS only if passes > 1
   return g;
@@ -129,10 +132,25 @@ __global__ void __launch_bounds__(64) zmpc_rollout_unc_kernel(
   // one 16-B (x, y) sample per lane from each bound array: coalesced 1 KiB per instruction
   const double2* zmx = reinterpret_cast<const double2*>(zmax + b * bstride);
   const double2* zmn = reinterpret_cast<const double2*>(zmin + b * bstride);
-  for (int t = lane; t < ((dbg & 8) ? 0 : n); t += 64) {
-    const double2 hi = zmx[t], lo = zmn[t];
-    zr0[ZL::idx(t)] = (hi.x + lo.x) / 2;  // z_ref = (z_max + z_min) / 2
-    zr1[ZL::idx(t)] = (hi.y + lo.y) / 2;
+  constexpr int kU = 8;  // 16 KiB of bound loads in flight per wave before the first use
+  for (int t0 = 0; t0 < ((dbg & 8) ? 0 : n); t0 += 64 * kU) {
+    double2 hi[kU], lo[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int t = t0 + u * 64 + lane;
+      if (t < n) {
+        hi[u] = zmx[t];
+        lo[u] = zmn[t];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int t = t0 + u * 64 + lane;
+      if (t < n) {
+        zr0[ZL::idx(t)] = (hi[u].x + lo[u].x) / 2;  // z_ref = (z_max + z_min) / 2
+        zr1[ZL::idx(t)] = (hi[u].y + lo[u].y) / 2;
+      }
+    }
   }
   {
     const double2 hi = zmx[n - 1], lo = zmn[n - 1];
@@ -265,42 +283,66 @@ __global__ void __launch_bounds__(64) zmpc_rollout_unc_kernel(
     y[i] = (lane == 0) ? xi1[i] : p1;
   }
 
-  // ---- 4. replay in the reference form x⁺ = A x + B u and store ---------------------
+  // ---- 4. replay in the reference form x⁺ = A x + B u; store through LDS ------------
+  // Lane l produces history rows l·C+1 .. l·C+C, i.e. 48-B pieces 48·C bytes apart across
+  // lanes; written directly that is one L2 request per lane per 16 B.  Instead the rows
+  // are staged in the (now dead) z_ref area, `rows_per_round` at a time, and copied out as
+  // contiguous 1-KiB wave stores; the cheap replay is recomputed once per round.
+  __syncthreads();
+  double* stage = smem;
+  const int rows_per_round = (2 * lzp) / 6;
   double* hb = hist + b * (int64_t)n * 6;
-  if (lane == 0) {
-    reinterpret_cast<double2*>(hb)[0] = make_double2(xi0[0], xi0[1]);
-    reinterpret_cast<double2*>(hb)[1] = make_double2(xi0[2], xi1[0]);
-    reinterpret_cast<double2*>(hb)[2] = make_double2(xi1[1], xi1[2]);
-  }
-  auto replay_step = [&](int m, double fx, double fy) {
-    const double ux = fx - (kx0 * x[0] + kx1 * x[1] + kx2 * x[2]);
-    const double uy = fy - (kx0 * y[0] + kx1 * y[1] + kx2 * y[2]);
-    double xn[3], yn[3];
-    lipm_step(lc, x, ux, xn);
-    lipm_step(lc, y, uy, yn);
-    if (m == kick_step) yn[1] -= kk;
-    if (!(dbg & 4)) {
-      double2* o = reinterpret_cast<double2*>(hb + (int64_t)(m + 1) * 6);
-      o[0] = make_double2(xn[0], xn[1]);
-      o[1] = make_double2(xn[2], yn[0]);
-      o[2] = make_double2(yn[1], yn[2]);
+  const double xs0[3] = {x[0], x[1], x[2]}, ys0[3] = {y[0], y[1], y[2]};
+  bool finite = true;
+  for (int r0 = 0; r0 < n; r0 += rows_per_round) {
+    const int r1 = min(r0 + rows_per_round, n);
+    if (lane == 0 && r0 == 0) {
+      stage[0] = xi0[0]; stage[1] = xi0[1]; stage[2] = xi0[2];
+      stage[3] = xi1[0]; stage[4] = xi1[1]; stage[5] = xi1[2];
     }
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      x[i] = xn[i];
-      y[i] = yn[i];
+      x[i] = xs0[i];
+      y[i] = ys0[i];
     }
-  };
-  if constexpr (REGF) {
+    auto replay_step = [&](int m, double fx, double fy) {
+      const double ux = fx - (kx0 * x[0] + kx1 * x[1] + kx2 * x[2]);
+      const double uy = fy - (kx0 * y[0] + kx1 * y[1] + kx2 * y[2]);
+      double xn[3], yn[3];
+      lipm_step(lc, x, ux, xn);
+      lipm_step(lc, y, uy, yn);
+      if (m == kick_step) yn[1] -= kk;
+      const int row = m + 1;
+      if (row >= r0 && row < r1) {
+        double* o = stage + (row - r0) * 6;
+        o[0] = xn[0]; o[1] = xn[1]; o[2] = xn[2];
+        o[3] = yn[0]; o[4] = yn[1]; o[5] = yn[2];
+      }
 #pragma unroll
-    for (int q = 0; q < CW; ++q)
-      if (mbeg + q < nsteps) replay_step(mbeg + q, a0[q], a1[q]);
-  } else {
-    for (int m = mbeg; m < min(mbeg + C, nsteps); ++m) replay_step(m, f0[m], f1[m]);
+      for (int i = 0; i < 3; ++i) {
+        x[i] = xn[i];
+        y[i] = yn[i];
+      }
+    };
+    if constexpr (REGF) {
+#pragma unroll
+      for (int q = 0; q < CW; ++q)
+        if (mbeg + q < nsteps) replay_step(mbeg + q, a0[q], a1[q]);
+    } else {
+      for (int m = mbeg; m < min(mbeg + C, nsteps); ++m) replay_step(m, f0[m], f1[m]);
+    }
+    __syncthreads();
+    if (!(dbg & 4)) {
+      const int nd2 = (r1 - r0) * 3;  // double2 items
+      const double2* src = reinterpret_cast<const double2*>(stage);
+      double2* dst = reinterpret_cast<double2*>(hb + (int64_t)r0 * 6);
+      for (int e = lane; e < nd2; e += 64) dst[e] = src[e];
+    }
+    __syncthreads();
   }
   if (status != nullptr) {
-    const bool finite = isfinite(x[0]) && isfinite(x[1]) && isfinite(x[2]) &&
-                        isfinite(y[0]) && isfinite(y[1]) && isfinite(y[2]);
+    finite = isfinite(x[0]) && isfinite(x[1]) && isfinite(x[2]) && isfinite(y[0]) &&
+             isfinite(y[1]) && isfinite(y[2]);
     const unsigned long long bad = __ballot(!finite);
     if (lane == 0) status[b] = bad ? ZMPC_ST_NONFINITE : 0;
   }

@@ -13,4 +13,8 @@ rc=$?; echo "ablate rc=$rc"; cat "$OUT/ablate.jsonl"
 [ $rc -ne 0 ] && exit $rc
 timeout -k 10 600 python bench.py --cpu-seconds 3 > "$OUT/bench.json" 2> "$OUT/bench.err"
 rc=$?; echo "bench rc=$rc"; cat "$OUT/bench.json"; tail -3 "$OUT/bench.err"
+
+[ $rc -ne 0 ] && exit $rc
+timeout -k 10 600 python bench.py --strict --batch ${STRICT_B:-8192} --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/bench_strict.json" 2> "$OUT/bench_strict.err"
+rc=$?; echo "bench strict rc=$rc"; cat "$OUT/bench_strict.json"; tail -3 "$OUT/bench_strict.err"
 exit $rc
