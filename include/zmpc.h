@@ -68,7 +68,8 @@ int zmpc_plan_destroy(zmpc_plan* plan);
 
 /* Plan quantities copied to HOST memory for inspection/tests.
  * what: 0 = p (N), 1 = Px (N*3, row-major), 2 = M (N*N), 3 = gain k (N), 4 = kx (3),
- *       5 = G (N*N, strict plans only), 6 = Cholesky factor L of M (N*N, lower).
+ *       5 = G (N*N, strict plans only), 6 = Cholesky factor L of M (N*N, lower),
+ *       7 = Hz = Q·I + R·Pu⁻ᵀPu⁻¹ = G⁻¹ (N*N, strict plans only).
  * count = number of doubles dst can hold; must be >= the quantity's size. */
 int zmpc_plan_export(const zmpc_plan* plan, int32_t what, double* dst_host, int64_t count);
 

@@ -35,7 +35,7 @@ struct DeviceGuard {
 
 void free_plan(zmpc_plan* p) {
   if (!p) return;
-  double* bufs[] = {p->p, p->Px, p->M, p->L, p->k, p->kx, p->X, p->G};
+  double* bufs[] = {p->p, p->Px, p->M, p->L, p->k, p->kx, p->X, p->G, p->v, p->Hz};
   for (double* b : bufs)
     if (b) (void)hipFree(b);
   if (p->info) (void)hipFree(p->info);
@@ -93,7 +93,8 @@ int zmpc_plan_create(int device, int32_t N, double T, double T2_2, double T3_6, 
     size_t n;
   } allocs[] = {{&P->p, (size_t)N},  {&P->Px, 3 * (size_t)N}, {&P->M, nn}, {&P->L, nn},
                 {&P->k, (size_t)P->Kpad + 64}, {&P->kx, 4},
-                {&P->X, strict ? nn : 0}, {&P->G, strict ? nn : 0}};
+                {&P->X, strict ? nn : 0}, {&P->G, strict ? nn : 0},
+                {&P->v, strict ? (size_t)N : 0}, {&P->Hz, strict ? nn : 0}};
   for (auto& a : allocs) {
     if (a.n == 0) continue;
     if ((e = hipMalloc((void**)a.ptr, a.n * sizeof(double))) != hipSuccess) {
@@ -166,6 +167,7 @@ int zmpc_plan_export(const zmpc_plan* P, int32_t what, double* dst, int64_t coun
     case 4: src = P->kx; n = 3; break;
     case 5: src = P->G; n = P->G ? N * N : 0; break;
     case 6: src = P->L; n = N * N; break;
+    case 7: src = P->Hz; n = P->Hz ? N * N : 0; break;
     default: return fail(ZMPC_EINVAL, "unknown export id");
   }
   if (!src || n == 0) return fail(ZMPC_ESTATE, "quantity not held by this plan");

@@ -41,6 +41,14 @@ struct PuOp {  // Pu[k][a] = p(k-a) for k >= a
   }
   __device__ int kbegin(int a0, int b0) const { return (a0 > b0 ? a0 : b0) & ~3; }
 };
+struct ToeplitzOp {  // lower-triangular Toeplitz T[k][a] = c(k-a) for k >= a (Pu, or Pu⁻¹)
+  const double* c;
+  int N;
+  __device__ double operator()(int k, int a) const {
+    return (k < N && a < N && k >= a) ? c[k - a] : 0.0;
+  }
+  __device__ int kbegin(int a0, int b0) const { return (a0 > b0 ? a0 : b0) & ~3; }
+};
 struct DenseOp {  // X[k][a], row-major N×N
   const double* X;
   int N;
@@ -193,6 +201,31 @@ __global__ void zmpc_solve_LPuT(int N, const double* __restrict__ L, const doubl
   }
 }
 
+// 5b. v = first column of Pu⁻¹ (lower-triangular Toeplitz again): p * v = e0, one thread.
+__global__ void zmpc_toeplitz_inverse(int N, const double* __restrict__ p,
+                                      double* __restrict__ v) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  const double p0 = p[0];
+  v[0] = 1.0 / p0;
+  for (int k = 1; k < N; ++k) {
+    double s = 0.0;
+    for (int j = 1; j <= k; ++j) s = fma(p[j], v[k - j], s);
+    v[k] = -s / p0;
+  }
+}
+
+template <class Op>
+static void launch_gram(int N, Op op, double alpha, double diag, double* C, hipStream_t s) {
+  if (N >= 64) {
+    const int tiles = (N + 15) / 16;
+    hipLaunchKernelGGL(zmpc_gram_mfma<Op>, dim3(tiles * tiles), dim3(64), 0, s, N, op, alpha,
+                       diag, C);
+  } else {
+    hipLaunchKernelGGL(zmpc_gram_fma<Op>, dim3((N * N + 255) / 256), dim3(256), 0, s, N, op,
+                       alpha, diag, C);
+  }
+}
+
 static hipError_t launch_gram_pu(const zmpc_plan* P, double diag, hipStream_t s) {
   PuOp op{P->p, P->N};
   const int N = P->N;
@@ -237,6 +270,11 @@ hipError_t zmpc_launch_plan(zmpc_plan* P, hipStream_t s) {
       hipLaunchKernelGGL(zmpc_gram_fma<DenseOp>, dim3((N * N + 255) / 256), dim3(256), 0, s, N,
                          op, 1.0 / P->Q, 0.0, P->G);
     }
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    // z-space Hessian H = Q·I + R·Pu⁻ᵀPu⁻¹ for the primal side of the strict active set
+    hipLaunchKernelGGL(zmpc_toeplitz_inverse, dim3(1), dim3(64), 0, s, N, P->p, P->v);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    launch_gram(N, ToeplitzOp{P->v, N}, P->R, P->Q, P->Hz, s);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   return hipSuccess;

@@ -33,14 +33,15 @@ constexpr int SMAXIT = 64;         // PDAS iteration cap
 
 struct StrictArgs {
   int N, Np, ld;         // horizon, padded to 16, W/D leading dimension
-  int mcap;              // largest |A| factored in LDS
+  int pcap;              // LDS doubles for the packed reduced factor
   int window_mode;       // 0 = rollout over [B,n,2] bounds, 1 = single step on [B,N] windows
   int64_t n;             // samples per walk (rollout)
   int64_t bstride;       // doubles between walks' bound arrays (0 = shared CoP)
   int64_t ninst;         // instances: 2B (rollout) or B (step)
   double Q, p0;
   LipmConsts lc;
-  const double* G;       // [N,N]
+  const double* G;       // [N,N] inverse z-space Hessian
+  const double* Hz;      // [N,N] z-space Hessian Q I + R Pu⁻ᵀPu⁻¹
   const double* Px;      // [N,3]
   const double* zmax;
   const double* zmin;
@@ -90,22 +91,42 @@ __device__ void build_w(const StrictArgs& a, int64_t inst, int64_t i, const doub
   }
 }
 
-// In-place lower Cholesky of the m×m matrix S (leading dimension m) by one wave.
+// Reduced-system factor storage: packed lower triangle in LDS (i(i+1)/2 + j) or a dense
+// m×m block in the wave's global scratch when it does not fit.
+template <bool PACKED>
+struct Tri {
+  double* S;
+  int m;
+  __device__ __forceinline__ double& at(int i, int j) const {
+    return PACKED ? S[(i * (i + 1) >> 1) + j] : S[i * m + j];
+  }
+};
+
+// In-place lower Cholesky of the SPD m×m matrix held in T (lower part), by one wave.  The
+// trailing update walks 8×8 blocks of the lower triangle (lane = (row, col) in the block),
+// so each column step costs ⌈r/8⌉(⌈r/8⌉+1)/2 wave instructions for r trailing rows.
 // Returns false if a pivot is not positive.
-__device__ bool wave_cholesky(double* S, int m, int lane) {
+template <bool PACKED>
+__device__ bool wave_cholesky(const Tri<PACKED>& T, int lane) {
+  const int m = T.m;
+  const int li = lane >> 3, lj = lane & 7;
   for (int k = 0; k < m; ++k) {
-    const double d = S[k * m + k];
+    const double d = T.at(k, k);
     if (!(d > 0.0)) return false;
     const double piv = sqrt(d);
     const double inv = 1.0 / piv;
     wave_sync();
-    for (int i = k + 1 + lane; i < m; i += 64) S[i * m + k] *= inv;
-    if (lane == 0) S[k * m + k] = piv;
+    for (int i = k + 1 + lane; i < m; i += 64) T.at(i, k) *= inv;
+    if (lane == 0) T.at(k, k) = piv;
     wave_sync();
     const int r = m - k - 1;
-    for (int t = lane; t < r * r; t += 64) {
-      const int i = k + 1 + t / r, j = k + 1 + t % r;
-      if (j <= i) S[i * m + j] -= S[i * m + k] * S[j * m + k];
+    const int nb = (r + 7) >> 3;
+    for (int bi = 0; bi < nb; ++bi) {
+      const int i = k + 1 + 8 * bi + li;
+      for (int bj = 0; bj <= bi; ++bj) {
+        const int j = k + 1 + 8 * bj + lj;
+        if (i < m && j <= i) T.at(i, j) -= T.at(i, k) * T.at(j, k);
+      }
     }
     wave_sync();
   }
@@ -113,18 +134,20 @@ __device__ bool wave_cholesky(double* S, int m, int lane) {
 }
 
 // Solve (L Lᵀ) v = rhs in place (rhs in v), L from wave_cholesky.
-__device__ void wave_chol_solve(const double* S, int m, double* v, int lane) {
+template <bool PACKED>
+__device__ void wave_chol_solve(const Tri<PACKED>& T, double* v, int lane) {
+  const int m = T.m;
   for (int j = 0; j < m; ++j) {
-    const double yj = v[j] / S[j * m + j];
+    const double yj = v[j] / T.at(j, j);
     wave_sync();
-    for (int i = j + 1 + lane; i < m; i += 64) v[i] -= S[i * m + j] * yj;
+    for (int i = j + 1 + lane; i < m; i += 64) v[i] -= T.at(i, j) * yj;
     if (lane == 0) v[j] = yj;
     wave_sync();
   }
   for (int j = m - 1; j >= 0; --j) {
-    const double yj = v[j] / S[j * m + j];
+    const double yj = v[j] / T.at(j, j);
     wave_sync();
-    for (int i = lane; i < j; i += 64) v[i] -= S[j * m + i] * yj;
+    for (int i = lane; i < j; i += 64) v[i] -= T.at(j, i) * yj;
     if (lane == 0) v[j] = yj;
     wave_sync();
   }
@@ -136,17 +159,46 @@ struct WaveWork {
   double* lo;    // [Np] z_min − c
   double* hi;    // [Np] z_max − c
   double* nuf;   // [Np] multipliers scattered to horizon slots
-  double* nuc;   // [Np] compact right-hand side / multipliers
-  int* idx;      // [Np] compact active indices
-  double* S;     // [mcap*mcap] LDS factor workspace
+  double* nuc;   // [Np] compact right-hand side / solution
+  int* ia;       // [Np] compact active slots
+  int* iff;      // [Np] compact free slots
+  double* S;     // packed LDS factor workspace (pcap doubles)
   double* Sg;    // [N*N] global factor scratch
 };
 
 constexpr int SNJ = 8;  // horizon slots per lane (N <= 512)
 
+// Factor the reduced matrix gathered by `gather(r, c)` (size m) and solve in place on w.nuc.
+template <class Gather>
+__device__ bool reduced_solve(const StrictArgs& a, const WaveWork& w, int m, Gather gather,
+                              int lane) {
+  if (m * (m + 1) / 2 <= a.pcap) {
+    Tri<true> T{w.S, m};
+    for (int r = lane; r < m; r += 64)
+      for (int c = 0; c <= r; ++c) T.at(r, c) = gather(r, c);
+    wave_sync();
+    if (!wave_cholesky(T, lane)) return false;
+    wave_chol_solve(T, w.nuc, lane);
+  } else {
+    Tri<false> T{w.Sg, m};
+    for (int t = lane; t < m * m; t += 64) {
+      const int r = t / m, c = t % m;
+      if (c <= r) T.at(r, c) = gather(r, c);
+    }
+    wave_sync();
+    if (!wave_cholesky(T, lane)) return false;
+    wave_chol_solve(T, w.nuc, lane);
+  }
+  return true;
+}
+
 // One strict QP solve for one instance.  D holds Q·G(z_ref − c) on entry; st is the
 // instance's warm-start status array (0 free, 1 upper, 2 lower), updated in place.
-// Returns u0 and ORs failure flags into *flags.
+// Each primal-dual active-set iteration solves the reduced KKT system on the smaller side:
+//   dual   (|A| <= |F|):  G_AA ν_A = (z* − t)_A,            z = z* − G_{:,A} ν_A
+//   primal (|A| >  |F|):  H_FF z_F = W_F − H_FA t_A (H = G⁻¹, W = Q(z_ref − c)),
+//                         ν_A = W_A − (H z)_A
+// (all in coordinates relative to c = Px x).  Returns u0; ORs failure flags into *flags.
 __device__ double solve_instance(const StrictArgs& a, int64_t inst, int64_t i, const double* x,
                                  const double* D, signed char* st, const WaveWork& w, int lane,
                                  int* flags) {
@@ -154,7 +206,6 @@ __device__ double solve_instance(const StrictArgs& a, int64_t inst, int64_t i, c
   for (int j = lane; j < N; j += 64) {
     const int64_t e = bound_index(a, inst, i, j);
     const double c = a.Px[3 * j] * x[0] + a.Px[3 * j + 1] * x[1] + a.Px[3 * j + 2] * x[2];
-    // bounds relative to c: z − c is the working variable (u0 needs z_0 − c_0)
     w.hi[j] = a.zmax[e] - c;
     w.lo[j] = a.zmin[e] - c;
     w.zs[j] = D[j];
@@ -165,42 +216,81 @@ __device__ double solve_instance(const StrictArgs& a, int64_t inst, int64_t i, c
   const double tolz = 1e-13, tolnu = 1e-13;
   bool done = false;
   for (int it = 0; it < SMAXIT; ++it) {
-    // compact the active set
-    int m = 0;
+    // compact the active and the free slots
+    int m = 0, f = 0;
     for (int j0 = 0; j0 < N; j0 += 64) {
       const int j = j0 + lane;
       const bool act = (j < N) && st[j] != 0;
-      const unsigned long long bal = __ballot(act);
-      const int pos = m + __popcll(bal & ((1ull << lane) - 1ull));
-      if (act) w.idx[pos] = j;
-      m += __popcll(bal);
+      const bool fre = (j < N) && st[j] == 0;
+      const unsigned long long ba = __ballot(act), bf = __ballot(fre);
+      const unsigned long long below = (1ull << lane) - 1ull;
+      if (act) w.ia[m + __popcll(ba & below)] = j;
+      if (fre) w.iff[f + __popcll(bf & below)] = j;
+      m += __popcll(ba);
+      f += __popcll(bf);
     }
     wave_sync();
-    if (m > 0) {
-      double* S = (m <= a.mcap) ? w.S : w.Sg;
-      for (int t = lane; t < m * m; t += 64) {
-        const int r = t / m, c = t % m;
-        S[t] = a.G[(size_t)w.idx[r] * N + w.idx[c]];
+    if (m == 0) {
+      for (int j = lane; j < N; j += 64) {
+        w.zz[j] = w.zs[j];
+        w.nuf[j] = 0.0;
       }
+    } else if (m <= f) {
+      // dual: G_AA ν = z*_A − t_A
       for (int r = lane; r < m; r += 64) {
-        const int j = w.idx[r];
+        const int j = w.ia[r];
         w.nuc[r] = w.zs[j] - (st[j] == 1 ? w.hi[j] : w.lo[j]);
       }
       wave_sync();
-      if (!wave_cholesky(S, m, lane)) {
+      const int* ia = w.ia;
+      const double* G = a.G;
+      if (!reduced_solve(a, w, m, [&](int r, int c) { return G[(size_t)ia[r] * N + ia[c]]; },
+                         lane)) {
         *flags |= ZMPC_ST_FACTOR;
         break;
       }
-      wave_chol_solve(S, m, w.nuc, lane);
-      for (int r = lane; r < m; r += 64) w.nuf[w.idx[r]] = w.nuc[r];
-      // z − c = D − G_{:,A} ν_A   (G symmetric: row idx_r is column idx_r)
+      for (int j = lane; j < N; j += 64) w.nuf[j] = 0.0;
+      wave_sync();
+      for (int r = lane; r < m; r += 64) w.nuf[w.ia[r]] = w.nuc[r];
+      // z − c = D − G_{:,A} ν_A   (G symmetric: row ia_r is column ia_r)
       for (int j = lane; j < N; j += 64) {
         double s = w.zs[j];
-        for (int r = 0; r < m; ++r) s -= a.G[(size_t)w.idx[r] * N + j] * w.nuc[r];
+        for (int r = 0; r < m; ++r) s -= a.G[(size_t)w.ia[r] * N + j] * w.nuc[r];
         w.zz[j] = s;
       }
     } else {
-      for (int j = lane; j < N; j += 64) w.zz[j] = w.zs[j];
+      // primal: H_FF z_F = W_F − H_FA t_A
+      for (int j = lane; j < N; j += 64)
+        w.zz[j] = (st[j] == 1) ? w.hi[j] : ((st[j] == 2) ? w.lo[j] : 0.0);
+      wave_sync();
+      for (int r = lane; r < f; r += 64) {
+        const int j = w.iff[r];
+        const double* Hj = a.Hz + (size_t)j * N;
+        double s = a.Q * ((w.hi[j] + w.lo[j]) / 2);  // W_j = Q (z_ref − c)_j
+        for (int q = 0; q < m; ++q) s -= Hj[w.ia[q]] * w.zz[w.ia[q]];
+        w.nuc[r] = s;
+      }
+      wave_sync();
+      const int* iff = w.iff;
+      const double* H = a.Hz;
+      if (f > 0 &&
+          !reduced_solve(a, w, f, [&](int r, int c) { return H[(size_t)iff[r] * N + iff[c]]; },
+                         lane)) {
+        *flags |= ZMPC_ST_FACTOR;
+        break;
+      }
+      for (int r = lane; r < f; r += 64) w.zz[w.iff[r]] = w.nuc[r];
+      wave_sync();
+      // ν = W − H z on the active slots, 0 on the free ones
+      for (int j = lane; j < N; j += 64) w.nuf[j] = 0.0;
+      wave_sync();
+      for (int q = lane; q < m; q += 64) {
+        const int j = w.ia[q];
+        const double* Hj = a.Hz + (size_t)j * N;
+        double s = a.Q * ((w.hi[j] + w.lo[j]) / 2);
+        for (int t = 0; t < N; ++t) s -= Hj[t] * w.zz[t];
+        w.nuf[j] = s;
+      }
     }
     wave_sync();
     // primal-dual set update: release active slots with wrong-signed multipliers, activate
@@ -235,10 +325,7 @@ __device__ double solve_instance(const StrictArgs& a, int64_t inst, int64_t i, c
 #pragma unroll
     for (int c = 0; c < SNJ; ++c) {
       const int j = lane + 64 * c;
-      if (j < N) {
-        st[j] = ns[c];
-        w.nuf[j] = 0.0;
-      }
+      if (j < N) st[j] = ns[c];
     }
     wave_sync();
   }
@@ -253,12 +340,12 @@ __global__ void __launch_bounds__(256) zmpc_strict_kernel(StrictArgs a) {
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int Np = a.Np, ld = a.ld;
   // LDS carve: Wt [SNB][ld] | xs [SNB][4] | flags [SNB] (as doubles) |
-  //            per wave {zs,zz,lo,hi,nuf,nuc}[Np], idx[Np] ints, S[mcap²] | st [SNB][Np] bytes
+  //            per wave {zs,zz,lo,hi,nuf,nuc}[Np], ia/iff[Np] ints, S[pcap] | st [SNB][Np] B
   double* Wt = smem;
   double* xs = Wt + SNB * ld;
   int* fl = reinterpret_cast<int*>(xs + SNB * 4);
   double* wbase = xs + SNB * 4 + SNB;
-  const int per_wave = 6 * Np + Np / 2 + a.mcap * a.mcap;
+  const int per_wave = 7 * Np + a.pcap;
   double* my = wbase + wave * per_wave;
   WaveWork w;
   w.zs = my;
@@ -267,8 +354,9 @@ __global__ void __launch_bounds__(256) zmpc_strict_kernel(StrictArgs a) {
   w.hi = my + 3 * Np;
   w.nuf = my + 4 * Np;
   w.nuc = my + 5 * Np;
-  w.idx = reinterpret_cast<int*>(my + 6 * Np);
-  w.S = my + 6 * Np + Np / 2;
+  w.ia = reinterpret_cast<int*>(my + 6 * Np);
+  w.iff = w.ia + Np;
+  w.S = my + 7 * Np;
   w.Sg = a.scratch + ((size_t)blockIdx.x * SWAVES + wave) * (size_t)a.N * a.N;
   signed char* stall = reinterpret_cast<signed char*>(wbase + SWAVES * per_wave);
 
@@ -310,11 +398,20 @@ __global__ void __launch_bounds__(256) zmpc_strict_kernel(StrictArgs a) {
           const int rt = wave + SWAVES * t;
           if (rt < nrt) {
             const int row = rt * 16 + r;
-            for (int k0 = 0; k0 < Np; k0 += 4) {
-              const int k = k0 + kq;
-              const double gv = (row < a.N && k < a.N) ? a.G[(size_t)k * a.N + row] : 0.0;
-              const double wv = Wt[r * ld + k];
-              acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(gv, wv, acc[t], 0, 0, 0);
+            const double* Gr = a.G + row;
+            const bool rok = row < a.N;
+            // Np is a multiple of 16: four k-steps per group, loads issued before the MFMAs
+            for (int k0 = 0; k0 < Np; k0 += 16) {
+              double gv[4], wv[4];
+#pragma unroll
+              for (int u = 0; u < 4; ++u) {
+                const int k = k0 + 4 * u + kq;
+                gv[u] = (rok && k < a.N) ? Gr[(size_t)k * a.N] : 0.0;
+                wv[u] = Wt[r * ld + k];
+              }
+#pragma unroll
+              for (int u = 0; u < 4; ++u)
+                acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(gv[u], wv[u], acc[t], 0, 0, 0);
             }
           }
         }
@@ -390,8 +487,8 @@ __global__ void __launch_bounds__(256) zmpc_strict_kernel(StrictArgs a) {
   }
 }
 
-size_t strict_lds_bytes(int Np, int ld, int mcap) {
-  const size_t per_wave = 6 * Np + Np / 2 + (size_t)mcap * mcap;
+size_t strict_lds_bytes(int Np, int ld, int pcap) {
+  const size_t per_wave = 7 * Np + (size_t)pcap;
   return (SNB * ld + SNB * 4 + SNB + SWAVES * per_wave) * sizeof(double) + SNB * Np;
 }
 
@@ -411,23 +508,29 @@ static hipError_t launch_strict(const zmpc_plan* p, StrictArgs a, hipStream_t s,
   a.N = p->N;
   a.Np = (p->N + 15) & ~15;
   a.ld = a.Np + 4;
-  int mcap = 48;
-  while (mcap > 0 && strict_lds_bytes(a.Np, a.ld, mcap) > 150 * 1024) mcap -= 8;
-  if (strict_lds_bytes(a.Np, a.ld, mcap) > 160 * 1024) {
+  // packed factor room for min(|A|, |F|) <= N/2 when it fits, else as much as fits
+  const size_t budget = 160 * 1024 - 512;
+  if (strict_lds_bytes(a.Np, a.ld, 0) > budget) {
     *why = "horizon too long for the strict solver's LDS tile (N=" + std::to_string(p->N) + ")";
     return hipErrorInvalidValue;
   }
-  a.mcap = mcap;
+  const int half = p->N / 2;
+  int pcap = half * (half + 1) / 2;
+  const size_t fixed = strict_lds_bytes(a.Np, a.ld, 0);
+  const int fit = (int)((budget - fixed) / (SWAVES * sizeof(double)));
+  if (pcap > fit) pcap = fit;
+  a.pcap = pcap & ~1;
   a.Q = p->Q;
   a.lc = p->lc;
   a.G = p->G;
+  a.Hz = p->Hz;
   a.Px = p->Px;
   // p(0) = T³/6·1 − T h/g  (zmp_controller.py:171 with i = j)
   a.p0 = p->T3_6 - p->Thg;
   const int64_t ntiles = (a.ninst + SNB - 1) / SNB;
   int grid = (int)std::min<int64_t>(ntiles, (int64_t)p->strict_slots);
   a.scratch = p->scratch;
-  const size_t lds = strict_lds_bytes(a.Np, a.ld, a.mcap);
+  const size_t lds = strict_lds_bytes(a.Np, a.ld, a.pcap);
   hipLaunchKernelGGL(zmpc_strict_kernel, dim3(grid), dim3(256), lds, s, a);
   return hipGetLastError();
 }

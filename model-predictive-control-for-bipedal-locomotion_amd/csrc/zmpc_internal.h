@@ -32,6 +32,8 @@ struct zmpc_plan {
   double* kx = nullptr;  // [3]  k·Px
   double* X = nullptr;   // [N,N] L⁻¹ Puᵀ (strict plans)
   double* G = nullptr;   // [N,N] Pu (R I + Q PuᵀPu)⁻¹ Puᵀ (strict plans)
+  double* v = nullptr;   // [N]   first column of Pu⁻¹ (strict plans)
+  double* Hz = nullptr;  // [N,N] Q I + R Pu⁻ᵀPu⁻¹ = G⁻¹ (strict plans)
   int* info = nullptr;   // [1] factorisation status
   // strict solver: persistent-grid slots and their per-wave factor scratch
   int strict_slots = 0;

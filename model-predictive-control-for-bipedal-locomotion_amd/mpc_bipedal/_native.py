@@ -22,7 +22,7 @@ ST_MAXITER = 1
 ST_NONFINITE = 2
 ST_FACTOR = 4
 
-EXPORT_P, EXPORT_PX, EXPORT_M, EXPORT_K, EXPORT_KX, EXPORT_G, EXPORT_L = range(7)
+EXPORT_P, EXPORT_PX, EXPORT_M, EXPORT_K, EXPORT_KX, EXPORT_G, EXPORT_L, EXPORT_HZ = range(8)
 
 # every symbol include/zmpc.h declares, with (restype, argtypes)
 _c_dbl_p = ctypes.c_void_p  # device pointers travel as integers

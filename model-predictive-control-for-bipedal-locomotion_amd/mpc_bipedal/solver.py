@@ -61,14 +61,14 @@ class Plan:
 
     def export(self, what: int) -> np.ndarray:
         n = {0: self.N, 1: 3 * self.N, 2: self.N ** 2, 3: self.N, 4: 3, 5: self.N ** 2,
-             6: self.N ** 2}[what]
+             6: self.N ** 2, 7: self.N ** 2}[what]
         buf = np.empty(n, dtype=np.float64)
         rc = _native.load().zmpc_plan_export(
             self._h, what, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), n)
         _native.check(rc, "zmpc_plan_export")
         if what in (1,):
             return buf.reshape(self.N, 3)
-        if what in (2, 5, 6):
+        if what in (2, 5, 6, 7):
             return buf.reshape(self.N, self.N)
         return buf
 

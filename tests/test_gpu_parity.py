@@ -53,6 +53,8 @@ def test_plan_matrices(N):
     Hz, V, _, _ = O.strict_matrices(N, dt, H, G, Q, R)
     Gref = np.linalg.inv(Hz)
     assert np.abs(Gd - Gref).max() <= 1e-10 * np.abs(Gref).max()
+    Hd = p.export(_native.EXPORT_HZ)
+    assert np.abs(Hd - Hz).max() <= 1e-10 * np.abs(Hz).max()
 
 
 @pytest.mark.parametrize("N", (10, 64, 150, 512))
