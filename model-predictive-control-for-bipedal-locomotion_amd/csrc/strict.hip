@@ -19,6 +19,9 @@
 //          L2 (batch-invariant, 176 KB at N=150), W/D tile in LDS;
 //   solve  each wave takes 4 instances: PDAS; G_AA Cholesky in LDS (in a per-wave global
 //          scratch when |A| is large), state advance, kick, history store, next W.
+#include <cstdio>
+#include <cstdlib>
+
 #include "zmpc_internal.h"
 
 namespace {
@@ -51,6 +54,23 @@ struct StrictArgs {
   double* out;           // rollout hist [B,n,2,3], step x_next [B,3]
   int32_t* status;       // [B] or null
   double* scratch;       // per-wave N*N factor scratch (gridDim*SWAVES slots)
+  unsigned long long* dbg;  // diagnostic phase counters (ZMPC_DEBUG_STRICT), null normally
+};
+
+// Diagnostic phase timer: only when a.dbg is set (a separate, opt-in run; never in the bench).
+struct PhaseClock {
+  unsigned long long* dbg;
+  unsigned long long t;
+  __device__ explicit PhaseClock(unsigned long long* d) : dbg(d), t(d ? __builtin_amdgcn_s_memtime() : 0) {}
+  __device__ void lap(int slot, int lane) {
+    if (!dbg) return;
+    const unsigned long long now = __builtin_amdgcn_s_memtime();
+    if (lane == 0) atomicAdd(dbg + slot, now - t);
+    t = now;
+  }
+  __device__ void count(int slot, unsigned long long v, int lane) {
+    if (dbg && lane == 0) atomicAdd(dbg + slot, v);
+  }
 };
 
 __device__ __forceinline__ void wave_sync() {
@@ -172,14 +192,20 @@ constexpr int SNJ = 8;  // horizon slots per lane (N <= 512)
 template <class Gather>
 __device__ bool reduced_solve(const StrictArgs& a, const WaveWork& w, int m, Gather gather,
                               int lane) {
+  PhaseClock clk(a.dbg);
+  clk.count(12, m, lane);
   if (m * (m + 1) / 2 <= a.pcap) {
     Tri<true> T{w.S, m};
     for (int r = lane; r < m; r += 64)
       for (int c = 0; c <= r; ++c) T.at(r, c) = gather(r, c);
     wave_sync();
+    clk.lap(2, lane);
     if (!wave_cholesky(T, lane)) return false;
+    clk.lap(3, lane);
     wave_chol_solve(T, w.nuc, lane);
+    clk.lap(4, lane);
   } else {
+    clk.count(14, 1, lane);
     Tri<false> T{w.Sg, m};
     for (int t = lane; t < m * m; t += 64) {
       const int r = t / m, c = t % m;
@@ -203,6 +229,7 @@ __device__ double solve_instance(const StrictArgs& a, int64_t inst, int64_t i, c
                                  const double* D, signed char* st, const WaveWork& w, int lane,
                                  int* flags) {
   const int N = a.N;
+  PhaseClock clk(a.dbg);
   for (int j = lane; j < N; j += 64) {
     const int64_t e = bound_index(a, inst, i, j);
     const double c = a.Px[3 * j] * x[0] + a.Px[3 * j + 1] * x[1] + a.Px[3 * j + 2] * x[2];
@@ -213,9 +240,12 @@ __device__ double solve_instance(const StrictArgs& a, int64_t inst, int64_t i, c
     w.nuf[j] = 0.0;
   }
   wave_sync();
+  clk.lap(0, lane);
+  clk.count(11, 1, lane);
   const double tolz = 1e-13, tolnu = 1e-13;
   bool done = false;
   for (int it = 0; it < SMAXIT; ++it) {
+    clk.count(9, 1, lane);
     // compact the active and the free slots
     int m = 0, f = 0;
     for (int j0 = 0; j0 < N; j0 += 64) {
@@ -230,6 +260,9 @@ __device__ double solve_instance(const StrictArgs& a, int64_t inst, int64_t i, c
       f += __popcll(bf);
     }
     wave_sync();
+    clk.lap(1, lane);
+    clk.count(10, m, lane);
+    if (m > f) clk.count(13, 1, lane);
     if (m == 0) {
       for (int j = lane; j < N; j += 64) {
         w.zz[j] = w.zs[j];
@@ -293,6 +326,7 @@ __device__ double solve_instance(const StrictArgs& a, int64_t inst, int64_t i, c
       }
     }
     wave_sync();
+    clk.lap(5, lane);
     // primal-dual set update: release active slots with wrong-signed multipliers, activate
     // violated free slots
     signed char ns[SNJ];
@@ -318,6 +352,7 @@ __device__ double solve_instance(const StrictArgs& a, int64_t inst, int64_t i, c
       }
     }
     changed = __any(changed);
+    clk.lap(6, lane);
     if (!changed) {
       done = true;
       break;
@@ -387,6 +422,7 @@ __global__ void __launch_bounds__(256) zmpc_strict_kernel(StrictArgs a) {
     __syncthreads();
 
     for (int64_t i = 0; i < nsteps; ++i) {
+      PhaseClock kclk(a.dbg);
       // ---- GEMM: D = G · W for the 16 instances of the tile (MFMA f64) ----------------
       dbl4 acc[SMAX_RT];
 #pragma unroll
@@ -428,6 +464,7 @@ __global__ void __launch_bounds__(256) zmpc_strict_kernel(StrictArgs a) {
       }
       __syncthreads();
 
+      kclk.lap(7, lane);
       // ---- per-instance active set, state advance, next W ------------------------------
       for (int q = 0; q < SPW; ++q) {
         const int s = wave * SPW + q;
@@ -468,7 +505,9 @@ __global__ void __launch_bounds__(256) zmpc_strict_kernel(StrictArgs a) {
         wave_sync();
         if (i + 1 < nsteps) build_w(a, inst, i + 1, xn, Wt + s * ld, lane);
       }
+      kclk.lap(8, lane);
       __syncthreads();
+      kclk.lap(15, lane);
     }
     // ---- status: OR over the axes of a walk -------------------------------------------
     if (a.status != nullptr) {
@@ -531,8 +570,28 @@ static hipError_t launch_strict(const zmpc_plan* p, StrictArgs a, hipStream_t s,
   int grid = (int)std::min<int64_t>(ntiles, (int64_t)p->strict_slots);
   a.scratch = p->scratch;
   const size_t lds = strict_lds_bytes(a.Np, a.ld, a.pcap);
+  static const bool dbg_on = getenv("ZMPC_DEBUG_STRICT") != nullptr;  // diagnostics only
+  static unsigned long long* dbgbuf = nullptr;
+  if (dbg_on && !dbgbuf) (void)hipMalloc((void**)&dbgbuf, 32 * sizeof(unsigned long long));
+  if (dbg_on && dbgbuf) {
+    (void)hipMemsetAsync(dbgbuf, 0, 32 * sizeof(unsigned long long), s);
+    a.dbg = dbgbuf;
+  }
   hipLaunchKernelGGL(zmpc_strict_kernel, dim3(grid), dim3(256), lds, s, a);
-  return hipGetLastError();
+  hipError_t e = hipGetLastError();
+  if (dbg_on && dbgbuf && e == hipSuccess) {
+    unsigned long long h[32];
+    (void)hipStreamSynchronize(s);
+    (void)hipMemcpy(h, dbgbuf, sizeof(h), hipMemcpyDeviceToHost);
+    fprintf(stderr,
+            "[zmpc strict dbg] grid=%d pcap=%d cycles: prep=%llu compact=%llu gather=%llu "
+            "chol=%llu cholsolve=%llu zupd=%llu setupd=%llu gemm=%llu inst_rest=%llu "
+            "barrier=%llu | solves=%llu iters=%llu sum_m=%llu primal=%llu sum_fact=%llu "
+            "global_fact=%llu\n",
+            grid, a.pcap, h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[15], h[11],
+            h[9], h[10], h[13], h[12], h[14]);
+  }
+  return e;
 }
 
 hipError_t zmpc_launch_rollout_strict(const zmpc_plan* p, int64_t B, int64_t n,
