@@ -11,14 +11,18 @@
 // in parallel (a sliding correlation), and only the 3-dim state recursion is sequential;
 // that recursion is run as a lane-parallel affine scan.
 //
-// Mapping: one 64-lane wavefront per walk (both axes).  Per wave:
-//   1. stage z_ref = (z_max + z_min)/2 (:197) for both axes in LDS, padded with the last row
-//      (:81-88), from coalesced loads of the walk's contiguous [n,2] bound rows;
-//   2. correlation with an 8-wide register sliding window; k streams from scalar loads
-//      (wave-uniform index) so each j costs one LDS read per axis for 8 FMAs;
-//   3. chunked affine scan over the 64 lanes with P = Ā^C (Ā = A - B kxᵀ), Kogge-Stone;
-//   4. each lane replays its chunk in the reference form x⁺ = A x + B u, applies the
-//      F_ext kick (:105-106) and stores the states.
+// Mapping: one 64-lane wavefront per walk at a time (both axes), persistent over walks.
+// Per walk:
+//   1. z_ref = (z_max + z_min)/2 (:197) for both axes staged in LDS, padded with the last row
+//      (:81-88); the bounds were loaded (16-B coalesced, whole walk in flight) into registers
+//      while the previous walk was being solved;
+//   2. correlation: lane l owns timesteps [l·CW, l·CW + CW), a CW-deep register sliding
+//      window, k from scalar loads (wave-uniform index): one LDS read per CW FMAs per axis;
+//   3. chunked affine scan over the 64 lanes with P = Ā^CW (Ā = A - B kxᵀ), Kogge-Stone;
+//   4. each lane replays its chunk in the reference form x⁺ = A x + B u with the F_ext kick
+//      (:105-106); history rows are staged in LDS and leave as contiguous 1-KiB wave stores,
+//      which drain while the next walk computes.
+#include <algorithm>
 #include <climits>
 #include <cstdint>
 #include <cstdlib>
@@ -56,11 +60,9 @@ __device__ __forceinline__ void lipm_step(const LipmConsts& c, const double* x, 
   y[2] = x[2] + c.T * u;
 }
 
-}  // namespace
-
 // Correlation tile width: outputs per lane per pass, chosen per walk length so that
 // passes·64·CW barely covers the n−1 timesteps (n = 420 → CW = 7: 448 outputs, 1 pass).
-static int pick_cw(int64_t nsteps) {
+int pick_cw(int64_t nsteps) {
   int best = 8;
   int64_t best_cost = INT64_MAX;
   for (int cw = 8; cw >= 1; --cw) {
@@ -83,9 +85,10 @@ struct ZrLayout {
 
 struct RolloutGeom {
   int cw, passes, kc, lz, lzp, nf;
+  int nbuf;  // z_ref buffers per wave: 2 (prefetching persistent kernel) or 1
 };
 
-static RolloutGeom rollout_geom(int N, int64_t n) {
+RolloutGeom rollout_geom(int N, int64_t n) {
   RolloutGeom g;
   const int64_t nsteps = n - 1;
   g.cw = pick_cw(nsteps);
@@ -98,118 +101,134 @@ static RolloutGeom rollout_geom(int N, int64_t n) {
   const int64_t stage_min = ((n + 1) / 2 * 6 + 1) / 2;
   if (g.lzp < stage_min) g.lzp = (int)stage_min;
   g.lzp = (g.lzp + 1) & ~1;
-  g.nf = g.passes == 1 ? 0 : (int)((nsteps + 2) & ~1LL);   // f lives in LDS only if passes > 1
+  g.nf = g.passes == 1 ? 0 : (int)((nsteps + 2) & ~1LL);  // f lives in LDS only if passes > 1
+  g.nbuf = g.passes == 1 ? 2 : 1;
   return g;
 }
 
-size_t zmpc_rollout_unc_lds_bytes(int N, int64_t n) {
-  const RolloutGeom g = rollout_geom(N, n);
-  return (size_t)(2 * g.lzp + 2 * g.nf) * sizeof(double);
+size_t lds_bytes(const RolloutGeom& g) {
+  return (size_t)(g.nbuf * 2 * g.lzp + 2 * g.nf) * sizeof(double);
 }
 
-// One wave per walk.  REGF (n − 1 <= 64·CW, a single correlation pass): lane l's CW
-// correlation outputs are exactly its scan chunk [l·CW, l·CW + CW), so f never leaves
-// registers; otherwise f goes through LDS and the scan chunk is ⌈(n−1)/64⌉.
-template <int CW, bool REGF>
-__global__ void __launch_bounds__(64) zmpc_rollout_unc_kernel(
-    int kc, int lz, int lzp, int n, LipmConsts lc, const double* __restrict__ k,
-    const double* __restrict__ kxp, const double* __restrict__ zmax,
-    const double* __restrict__ zmin, int64_t bstride, const double* __restrict__ x0,
-    const double* __restrict__ kick, int64_t kick_step, double* __restrict__ hist,
-    int32_t* __restrict__ status, int dbg) {
+struct RolloutArgs {
+  int kc, lz, lzp, n;
+  int64_t B;
+  LipmConsts lc;
+  const double* k;
+  const double* kx;
+  const double* zmax;
+  const double* zmin;
+  int64_t bstride;
+  const double* x0;
+  const double* kick;
+  int64_t kick_step;
+  double* hist;
+  int32_t* status;
+  int dbg;
+};
+
+// Bounds of one walk held in registers: PF rounds of 64 samples, one 16-B (x, y) pair of
+// each bound array per lane and round.
+template <int PF>
+struct BoundRegs {
+  double2 hi[PF], lo[PF];
+};
+
+template <int PF>
+__device__ __forceinline__ void load_bounds(const RolloutArgs& a, int64_t b, int lane,
+                                            BoundRegs<PF>& r) {
+  const double2* zmx = reinterpret_cast<const double2*>(a.zmax + b * a.bstride);
+  const double2* zmn = reinterpret_cast<const double2*>(a.zmin + b * a.bstride);
+#pragma unroll
+  for (int u = 0; u < PF; ++u) {
+    const int t = u * 64 + lane;
+    if (t < a.n) {
+      r.hi[u] = zmx[t];
+      r.lo[u] = zmn[t];
+    }
+  }
+}
+
+// z_ref = (z_max + z_min) / 2 into the (padded) LDS layout, then the last row repeated up to
+// lz (the window padding of zmp_controller.py:81-88).
+template <int CW, int PF>
+__device__ __forceinline__ void store_zref(const RolloutArgs& a, const BoundRegs<PF>& r,
+                                           double* zr0, double* zr1, int lane) {
   using ZL = ZrLayout<CW>;
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int64_t b = blockIdx.x;
-  const int lane = threadIdx.x;
-  const int nsteps = n - 1;
-  const int passes = REGF ? 1 : (nsteps + 64 * CW - 1) / (64 * CW);
-  double* zr0 = smem;
-  double* zr1 = smem + lzp;
-  double* f0 = smem + 2 * lzp;                 // LDS f (REGF == false only)
-  double* f1 = f0 + ((nsteps + 2) & ~1);
-
-  // ---- 1. z_ref for both axes, padded with the last row -------------------------------
-  // one 16-B (x, y) sample per lane from each bound array: coalesced 1 KiB per instruction
-  const double2* zmx = reinterpret_cast<const double2*>(zmax + b * bstride);
-  const double2* zmn = reinterpret_cast<const double2*>(zmin + b * bstride);
-  constexpr int kU = 8;  // 16 KiB of bound loads in flight per wave before the first use
-  for (int t0 = 0; t0 < ((dbg & 8) ? 0 : n); t0 += 64 * kU) {
-    double2 hi[kU], lo[kU];
 #pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int t = t0 + u * 64 + lane;
-      if (t < n) {
-        hi[u] = zmx[t];
-        lo[u] = zmn[t];
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < kU; ++u) {
-      const int t = t0 + u * 64 + lane;
-      if (t < n) {
-        zr0[ZL::idx(t)] = (hi[u].x + lo[u].x) / 2;  // z_ref = (z_max + z_min) / 2
-        zr1[ZL::idx(t)] = (hi[u].y + lo[u].y) / 2;
-      }
+  for (int u = 0; u < PF; ++u) {
+    const int t = u * 64 + lane;
+    if (t < a.n) {
+      zr0[ZL::idx(t)] = (r.hi[u].x + r.lo[u].x) / 2;
+      zr1[ZL::idx(t)] = (r.hi[u].y + r.lo[u].y) / 2;
     }
   }
-  {
-    const double2 hi = zmx[n - 1], lo = zmn[n - 1];
-    const double last0 = (hi.x + lo.x) / 2, last1 = (hi.y + lo.y) / 2;
-    for (int t = n + lane; t < lz; t += 64) {
-      zr0[ZL::idx(t)] = last0;
-      zr1[ZL::idx(t)] = last1;
+  // the last sample lives in lane (n-1)%64 of round (n-1)/64: broadcast it
+  const int ul = (a.n - 1) >> 6, ll = (a.n - 1) & 63;
+  double h0 = 0.0, h1 = 0.0, l0 = 0.0, l1 = 0.0;
+#pragma unroll
+  for (int u = 0; u < PF; ++u)
+    if (u == ul) {
+      h0 = r.hi[u].x;
+      h1 = r.hi[u].y;
+      l0 = r.lo[u].x;
+      l1 = r.lo[u].y;
     }
+  h0 = __shfl(h0, ll, 64);
+  h1 = __shfl(h1, ll, 64);
+  l0 = __shfl(l0, ll, 64);
+  l1 = __shfl(l1, ll, 64);
+  const double last0 = (h0 + l0) / 2, last1 = (h1 + l1) / 2;
+  for (int t = a.n + lane; t < a.lz; t += 64) {
+    zr0[ZL::idx(t)] = last0;
+    zr1[ZL::idx(t)] = last1;
   }
-  __syncthreads();
+}
 
-  // ---- 2. f_i = Σ_j k_j z_ref[i+1+j], CW outputs per lane, sliding register window ----
-  double a0[CW], a1[CW];
-  for (int pass = 0; pass < ((dbg & 1) ? 0 : passes); ++pass) {
-    const int i0 = pass * 64 * CW + lane * CW;
-    // i0 is a multiple of CW, so idx(i0 + c) = idx(i0) + idx(c): compile-time offsets
-    const double* z0 = zr0 + ZL::idx(i0);
-    const double* z1 = zr1 + ZL::idx(i0);
-    double w0[CW], w1[CW];
+// f for lane l's CW timesteps of one pass starting at i0 (both axes).
+template <int CW>
+__device__ __forceinline__ void correlate(const RolloutArgs& a, const double* zr0,
+                                          const double* zr1, int i0, double* a0, double* a1) {
+  using ZL = ZrLayout<CW>;
+  // i0 is a multiple of CW, so idx(i0 + c) = idx(i0) + idx(c): compile-time offsets
+  const double* z0 = zr0 + ZL::idx(i0);
+  const double* z1 = zr1 + ZL::idx(i0);
+  double w0[CW], w1[CW];
 #pragma unroll
-    for (int m = 0; m < CW; ++m) {
-      a0[m] = 0.0;
-      a1[m] = 0.0;
-      w0[m] = z0[ZL::idx(1 + m)];
-      w1[m] = z1[ZL::idx(1 + m)];
-    }
-    for (int j = 0; j < kc; j += CW) {
+  for (int m = 0; m < CW; ++m) {
+    a0[m] = 0.0;
+    a1[m] = 0.0;
+    w0[m] = z0[ZL::idx(1 + m)];
+    w1[m] = z1[ZL::idx(1 + m)];
+  }
+  const double* __restrict__ k = a.k;
+  for (int j = 0; j < a.kc; j += CW) {
 #pragma unroll
-      for (int jj = 0; jj < CW; ++jj) {
-        const double kj = k[j + jj];
-#pragma unroll
-        for (int m = 0; m < CW; ++m) {
-          a0[m] = fma(kj, w0[(jj + m) % CW], a0[m]);
-          a1[m] = fma(kj, w1[(jj + m) % CW], a1[m]);
-        }
-        w0[jj] = z0[ZL::idx(1 + jj + CW)];
-        w1[jj] = z1[ZL::idx(1 + jj + CW)];
-      }
-      z0 += CW + ZL::kPad;
-      z1 += CW + ZL::kPad;
-    }
-    if constexpr (!REGF) {
+    for (int jj = 0; jj < CW; ++jj) {
+      const double kj = k[j + jj];
 #pragma unroll
       for (int m = 0; m < CW; ++m) {
-        if (i0 + m < nsteps) {
-          f0[i0 + m] = a0[m];
-          f1[i0 + m] = a1[m];
-        }
+        a0[m] = fma(kj, w0[(jj + m) % CW], a0[m]);
+        a1[m] = fma(kj, w1[(jj + m) % CW], a1[m]);
       }
+      w0[jj] = z0[ZL::idx(1 + jj + CW)];
+      w1[jj] = z1[ZL::idx(1 + jj + CW)];
     }
+    z0 += CW + ZL::kPad;
+    z1 += CW + ZL::kPad;
   }
-  if (dbg & 1) {
-#pragma unroll
-    for (int m = 0; m < CW; ++m) a0[m] = a1[m] = 0.0;
-  }
-  if constexpr (!REGF) __syncthreads();
+}
 
-  // ---- 3. affine scan of x_{i+1} = Ā x_i + B f_i (+ kick) over 64 lane chunks ----------
-  const double kx0 = kxp[0], kx1 = kxp[1], kx2 = kxp[2];
+// Scan, replay and store of one walk whose f is in registers (REGF: a0/a1[q] = f of
+// timestep lane·CW + q) or in LDS (f0/f1).  `stage` (>= 2·lzp doubles) is free LDS.
+template <int CW, bool REGF>
+__device__ __forceinline__ void scan_replay_store(const RolloutArgs& a, int64_t b, int lane,
+                                                  const double* a0, const double* a1,
+                                                  const double* f0, const double* f1,
+                                                  double* stage) {
+  const int n = a.n, nsteps = n - 1;
+  const LipmConsts lc = a.lc;
+  const double kx0 = a.kx[0], kx1 = a.kx[1], kx2 = a.kx[2];
   const double Bv[3] = {lc.T3_6, lc.T2_2, lc.T};
   Mat3 Ab;  // Ā = A - B kxᵀ
   {
@@ -222,8 +241,10 @@ __global__ void __launch_bounds__(64) zmpc_rollout_unc_kernel(
   }
   const int C = REGF ? CW : (nsteps + 63) / 64;  // steps per lane chunk
   const int mbeg = lane * C;
-  const double kk = (kick != nullptr) ? kick[b] : 0.0;
+  const double kk = (a.kick != nullptr) ? a.kick[b] : 0.0;
+  const int64_t kick_step = a.kick_step;
 
+  // ---- 3. affine scan of x_{i+1} = Ā x_i + B f_i (+ kick) over 64 lane chunks ----------
   double s0[3] = {0.0, 0.0, 0.0}, s1[3] = {0.0, 0.0, 0.0};
   auto scan_step = [&](int m, double fx, double fy) {
     double t[3];
@@ -246,7 +267,7 @@ __global__ void __launch_bounds__(64) zmpc_rollout_unc_kernel(
   }
   Mat3 P = Ab;  // P = Ā^C
   for (int q = 1; q < C; ++q) P = matmul3(P, Ab);
-  const double* xb = x0 + b * 6;
+  const double* xb = a.x0 + b * 6;
   const double xi0[3] = {xb[0], xb[1], xb[2]};
   const double xi1[3] = {xb[3], xb[4], xb[5]};
   if (lane == 0) {
@@ -258,7 +279,7 @@ __global__ void __launch_bounds__(64) zmpc_rollout_unc_kernel(
   }
   // inclusive Kogge-Stone: T_l += P^d T_{l-d}
   Mat3 Pd = P;
-  for (int d = 1; d < ((dbg & 2) ? 1 : 64); d <<= 1) {
+  for (int d = 1; d < ((a.dbg & 2) ? 1 : 64); d <<= 1) {
     double u0[3], u1[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -286,19 +307,20 @@ __global__ void __launch_bounds__(64) zmpc_rollout_unc_kernel(
   // ---- 4. replay in the reference form x⁺ = A x + B u; store through LDS ------------
   // Lane l produces history rows l·C+1 .. l·C+C, i.e. 48-B pieces 48·C bytes apart across
   // lanes; written directly that is one L2 request per lane per 16 B.  Instead the rows
-  // are staged in the (now dead) z_ref area, `rows_per_round` at a time, and copied out as
-  // contiguous 1-KiB wave stores; the cheap replay is recomputed once per round.
-  __syncthreads();
-  double* stage = smem;
-  const int rows_per_round = (2 * lzp) / 6;
-  double* hb = hist + b * (int64_t)n * 6;
+  // are staged in LDS, `rows_per_round` at a time, and copied out as contiguous 1-KiB wave
+  // stores; the cheap replay is recomputed once per round.
+  const int rows_per_round = (2 * a.lzp) / 6;
+  double* hb = a.hist + b * (int64_t)n * 6;
   const double xs0[3] = {x[0], x[1], x[2]}, ys0[3] = {y[0], y[1], y[2]};
-  bool finite = true;
   for (int r0 = 0; r0 < n; r0 += rows_per_round) {
     const int r1 = min(r0 + rows_per_round, n);
     if (lane == 0 && r0 == 0) {
-      stage[0] = xi0[0]; stage[1] = xi0[1]; stage[2] = xi0[2];
-      stage[3] = xi1[0]; stage[4] = xi1[1]; stage[5] = xi1[2];
+      stage[0] = xi0[0];
+      stage[1] = xi0[1];
+      stage[2] = xi0[2];
+      stage[3] = xi1[0];
+      stage[4] = xi1[1];
+      stage[5] = xi1[2];
     }
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -315,8 +337,12 @@ __global__ void __launch_bounds__(64) zmpc_rollout_unc_kernel(
       const int row = m + 1;
       if (row >= r0 && row < r1) {
         double* o = stage + (row - r0) * 6;
-        o[0] = xn[0]; o[1] = xn[1]; o[2] = xn[2];
-        o[3] = yn[0]; o[4] = yn[1]; o[5] = yn[2];
+        o[0] = xn[0];
+        o[1] = xn[1];
+        o[2] = xn[2];
+        o[3] = yn[0];
+        o[4] = yn[1];
+        o[5] = yn[2];
       }
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
@@ -332,7 +358,7 @@ __global__ void __launch_bounds__(64) zmpc_rollout_unc_kernel(
       for (int m = mbeg; m < min(mbeg + C, nsteps); ++m) replay_step(m, f0[m], f1[m]);
     }
     __syncthreads();
-    if (!(dbg & 4)) {
+    if (!(a.dbg & 4)) {
       const int nd2 = (r1 - r0) * 3;  // double2 items
       const double2* src = reinterpret_cast<const double2*>(stage);
       double2* dst = reinterpret_cast<double2*>(hb + (int64_t)r0 * 6);
@@ -340,12 +366,107 @@ __global__ void __launch_bounds__(64) zmpc_rollout_unc_kernel(
     }
     __syncthreads();
   }
-  if (status != nullptr) {
-    finite = isfinite(x[0]) && isfinite(x[1]) && isfinite(x[2]) && isfinite(y[0]) &&
-             isfinite(y[1]) && isfinite(y[2]);
+  if (a.status != nullptr) {
+    const bool finite = isfinite(x[0]) && isfinite(x[1]) && isfinite(x[2]) &&
+                        isfinite(y[0]) && isfinite(y[1]) && isfinite(y[2]);
     const unsigned long long bad = __ballot(!finite);
-    if (lane == 0) status[b] = bad ? ZMPC_ST_NONFINITE : 0;
+    if (lane == 0) a.status[b] = bad ? ZMPC_ST_NONFINITE : 0;
   }
+}
+
+// Walks of at most 64·CW+1 samples (one correlation pass): persistent over walks, f in
+// registers, the next walk's bounds in flight in registers while this walk computes,
+// z_ref double-buffered in LDS (buffer A = this walk, B = next walk; A is the staging area
+// of this walk's history once its correlation is done).
+template <int CW>
+__global__ void __launch_bounds__(64) zmpc_rollout_unc_kernel(RolloutArgs a) {
+  constexpr int PF = CW + 1;  // 64·(CW+1) >= n
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int lane = threadIdx.x;
+  double* buf[2] = {smem, smem + 2 * a.lzp};
+  int cur = 0;
+  BoundRegs<PF> r;
+  int64_t b = blockIdx.x;
+  if (b < a.B && !(a.dbg & 8)) load_bounds<PF>(a, b, lane, r);
+  if (b < a.B) store_zref<CW, PF>(a, r, buf[cur], buf[cur] + a.lzp, lane);
+  for (; b < a.B; b += gridDim.x) {
+    const int64_t bn = b + gridDim.x;
+    if (bn < a.B && !(a.dbg & 8)) load_bounds<PF>(a, bn, lane, r);  // in flight meanwhile
+    __syncthreads();
+    double a0[CW], a1[CW];
+    if (!(a.dbg & 1)) {
+      correlate<CW>(a, buf[cur], buf[cur] + a.lzp, lane * CW, a0, a1);
+    } else {
+#pragma unroll
+      for (int m = 0; m < CW; ++m) a0[m] = a1[m] = 0.0;
+    }
+    // the next walk's z_ref goes to the other buffer before this walk's stores are issued
+    // (so waiting for its loads never waits for this walk's stores)
+    if (bn < a.B) store_zref<CW, PF>(a, r, buf[cur ^ 1], buf[cur ^ 1] + a.lzp, lane);
+    __syncthreads();
+    scan_replay_store<CW, true>(a, b, lane, a0, a1, nullptr, nullptr, buf[cur]);
+    cur ^= 1;
+  }
+}
+
+// Longer walks (several correlation passes): one walk per wave, f through LDS.
+template <int CW>
+__global__ void __launch_bounds__(64) zmpc_rollout_unc_long_kernel(RolloutArgs a) {
+  using ZL = ZrLayout<CW>;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int64_t b = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int n = a.n, nsteps = n - 1;
+  const int passes = (nsteps + 64 * CW - 1) / (64 * CW);
+  double* zr0 = smem;
+  double* zr1 = smem + a.lzp;
+  double* f0 = smem + 2 * a.lzp;
+  double* f1 = f0 + ((nsteps + 2) & ~1);
+  {
+    const double2* zmx = reinterpret_cast<const double2*>(a.zmax + b * a.bstride);
+    const double2* zmn = reinterpret_cast<const double2*>(a.zmin + b * a.bstride);
+    constexpr int kU = 8;
+    for (int t0 = 0; t0 < n; t0 += 64 * kU) {
+      double2 hi[kU], lo[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int t = t0 + u * 64 + lane;
+        if (t < n) {
+          hi[u] = zmx[t];
+          lo[u] = zmn[t];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int t = t0 + u * 64 + lane;
+        if (t < n) {
+          zr0[ZL::idx(t)] = (hi[u].x + lo[u].x) / 2;
+          zr1[ZL::idx(t)] = (hi[u].y + lo[u].y) / 2;
+        }
+      }
+    }
+    const double2 hi = zmx[n - 1], lo = zmn[n - 1];
+    const double last0 = (hi.x + lo.x) / 2, last1 = (hi.y + lo.y) / 2;
+    for (int t = n + lane; t < a.lz; t += 64) {
+      zr0[ZL::idx(t)] = last0;
+      zr1[ZL::idx(t)] = last1;
+    }
+  }
+  __syncthreads();
+  for (int pass = 0; pass < passes; ++pass) {
+    const int i0 = pass * 64 * CW + lane * CW;
+    double a0[CW], a1[CW];
+    correlate<CW>(a, zr0, zr1, i0, a0, a1);
+#pragma unroll
+    for (int m = 0; m < CW; ++m) {
+      if (i0 + m < nsteps) {
+        f0[i0 + m] = a0[m];
+        f1[i0 + m] = a1[m];
+      }
+    }
+  }
+  __syncthreads();
+  scan_replay_store<CW, false>(a, b, lane, nullptr, nullptr, f0, f1, smem);
 }
 
 // Batched predict_wieber_axis (strict=False): one wave per instance.
@@ -376,20 +497,26 @@ __global__ void __launch_bounds__(256) zmpc_step_unc_kernel(
   }
 }
 
+int g_cus = 0;  // CUs of the device the attributes were set on (grid sizing)
+
 template <int CW>
-static void launch_unc(const RolloutGeom& g, size_t lds, hipStream_t s, int64_t B, int64_t n,
-                       const zmpc_plan* p, const double* zmax, const double* zmin,
-                       int64_t bstride, const double* x0, const double* kick, int64_t kick_step,
-                       double* hist, int32_t* status, int dbg) {
-  if (g.passes == 1)
-    hipLaunchKernelGGL((zmpc_rollout_unc_kernel<CW, true>), dim3((unsigned)B), dim3(64), lds, s,
-                       g.kc, g.lz, g.lzp, (int)n, p->lc, p->k, p->kx, zmax, zmin, bstride, x0,
-                       kick, kick_step, hist, status, dbg);
-  else
-    hipLaunchKernelGGL((zmpc_rollout_unc_kernel<CW, false>), dim3((unsigned)B), dim3(64), lds,
-                       s, g.kc, g.lz, g.lzp, (int)n, p->lc, p->k, p->kx, zmax, zmin, bstride,
-                       x0, kick, kick_step, hist, status, dbg);
+void launch_unc(const RolloutGeom& g, size_t lds, hipStream_t s, const RolloutArgs& a) {
+  if (g.passes == 1) {
+    // enough waves to fill the chip (LDS admits 160 KiB / lds per CU), >= 2 walks per wave
+    // where the batch allows, so that every wave's second walk loads behind its first
+    const int per_cu = std::max<int>(1, std::min<int>(16, (int)((160 * 1024) / lds)));
+    const int64_t cap = (int64_t)std::max(g_cus, 1) * per_cu;
+    const int64_t grid = std::min<int64_t>(std::max<int64_t>((a.B + 1) / 2, 1), cap);
+    hipLaunchKernelGGL(zmpc_rollout_unc_kernel<CW>, dim3((unsigned)grid), dim3(64), lds, s, a);
+  } else {
+    hipLaunchKernelGGL(zmpc_rollout_unc_long_kernel<CW>, dim3((unsigned)a.B), dim3(64), lds, s,
+                       a);
+  }
 }
+
+}  // namespace
+
+size_t zmpc_rollout_unc_lds_bytes(int N, int64_t n) { return lds_bytes(rollout_geom(N, n)); }
 
 hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, const double* zmax,
                                    const double* zmin, int64_t bstride, const double* x0,
@@ -404,7 +531,7 @@ hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, con
     return hipSuccess;
   }
   const RolloutGeom g = rollout_geom(p->N, n);
-  const size_t lds = (size_t)(2 * g.lzp + 2 * g.nf) * sizeof(double);
+  const size_t lds = lds_bytes(g);
   if (lds > 160 * 1024) {
     *why = "walk too long for the LDS-resident rollout (n=" + std::to_string(n) + ")";
     return hipErrorInvalidValue;
@@ -413,11 +540,12 @@ hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, con
     const char* e = getenv("ZMPC_DEBUG_ROLLOUT");  // diagnostic ablation bits (0 in production)
     return e ? atoi(e) : 0;
   }();
+  RolloutArgs a{g.kc, g.lz, g.lzp, (int)n, B,    p->lc,     p->k,   p->kx, zmax,
+                zmin, bstride, x0,  kick,   kick_step, hist, status, dbg};
   switch (g.cw) {
-#define ZMPC_CW(C)                                                                          \
-  case C:                                                                                   \
-    launch_unc<C>(g, lds, s, B, n, p, zmax, zmin, bstride, x0, kick, kick_step, hist, status, \
-                  dbg);                                                                     \
+#define ZMPC_CW(C)               \
+  case C:                        \
+    launch_unc<C>(g, lds, s, a); \
     break;
     ZMPC_CW(1) ZMPC_CW(2) ZMPC_CW(3) ZMPC_CW(4) ZMPC_CW(5) ZMPC_CW(6) ZMPC_CW(7) ZMPC_CW(8)
 #undef ZMPC_CW
@@ -437,13 +565,16 @@ hipError_t zmpc_launch_step_unc(const zmpc_plan* p, int64_t B, const double* x,
 
 // The dynamic-LDS ceiling must be raised once per device for > 64 KiB requests.
 hipError_t zmpc_rollout_unc_set_attrs() {
-  hipError_t e = hipSuccess;
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess)
+    e = hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev);
 #define ZMPC_ATTR(C)                                                                        \
   if (e == hipSuccess)                                                                      \
-    e = hipFuncSetAttribute((const void*)zmpc_rollout_unc_kernel<C, true>,                 \
+    e = hipFuncSetAttribute((const void*)zmpc_rollout_unc_kernel<C>,                       \
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);       \
   if (e == hipSuccess)                                                                      \
-    e = hipFuncSetAttribute((const void*)zmpc_rollout_unc_kernel<C, false>,                \
+    e = hipFuncSetAttribute((const void*)zmpc_rollout_unc_long_kernel<C>,                  \
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   ZMPC_ATTR(1) ZMPC_ATTR(2) ZMPC_ATTR(3) ZMPC_ATTR(4) ZMPC_ATTR(5) ZMPC_ATTR(6) ZMPC_ATTR(7)
   ZMPC_ATTR(8)
