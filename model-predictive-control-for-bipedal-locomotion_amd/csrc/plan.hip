@@ -188,6 +188,40 @@ __global__ void __launch_bounds__(1024) zmpc_gain(int N, int Kpad, const double*
   }
 }
 
+// 4b. Scan matrices of the unconstrained rollout: Ā = A − B kxᵀ and, for C = 1..8,
+// (Ā^C)^(2^r), r = 0..5 (the lane-chunk propagators of the Kogge-Stone scan).  One thread.
+__global__ void zmpc_scan_matrices(double T, double T2_2, double T3_6,
+                                   const double* __restrict__ kx, double* __restrict__ out) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  const double A[9] = {1.0, T, T2_2, 0.0, 1.0, T, 0.0, 0.0, 1.0};
+  const double Bv[3] = {T3_6, T2_2, T};
+  double Ab[9];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) Ab[3 * i + j] = A[3 * i + j] - Bv[i] * kx[j];
+  auto mul = [](const double* x, const double* y, double* z) {
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j)
+        z[3 * i + j] = fma(x[3 * i + 0], y[0 + j], fma(x[3 * i + 1], y[3 + j], x[3 * i + 2] * y[6 + j]));
+  };
+  double P[9];
+  for (int q = 0; q < 9; ++q) P[q] = Ab[q];
+  for (int C = 1; C <= 8; ++C) {
+    if (C > 1) {
+      double t[9];
+      mul(P, Ab, t);
+      for (int q = 0; q < 9; ++q) P[q] = t[q];
+    }
+    double Q[9];
+    for (int q = 0; q < 9; ++q) Q[q] = P[q];
+    for (int r = 0; r < 6; ++r) {
+      for (int q = 0; q < 9; ++q) out[(C - 1) * 54 + r * 9 + q] = Q[q];
+      double t[9];
+      mul(Q, Q, t);
+      for (int q = 0; q < 9; ++q) Q[q] = t[q];
+    }
+  }
+}
+
 // 5a. X = L⁻¹ Puᵀ: one thread per column c, forward substitution with L broadcast across the
 // wave (every lane reads the same L element).  Puᵀ[i][c] = p(c-i) for i <= c.
 __global__ void zmpc_solve_LPuT(int N, const double* __restrict__ L, const double* __restrict__ p,
@@ -256,6 +290,9 @@ hipError_t zmpc_launch_plan(zmpc_plan* P, hipStream_t s) {
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(zmpc_gain, dim3(1), dim3(1024), sizeof(double) * N, s, N, P->Kpad, P->L,
                      P->p, P->Px, P->k, P->kx);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(zmpc_scan_matrices, dim3(1), dim3(64), 0, s, P->T, P->T2_2, P->T3_6, P->kx,
+                     P->scanP);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if (P->strict) {
     hipLaunchKernelGGL(zmpc_solve_LPuT, dim3((N + 63) / 64), dim3(64), 0, s, N, P->L, P->p,

@@ -11,17 +11,17 @@
 // in parallel (a sliding correlation), and only the 3-dim state recursion is sequential;
 // that recursion is run as a lane-parallel affine scan.
 //
-// Mapping: one 64-lane wavefront per walk at a time (both axes), persistent over walks.
-// Per walk:
-//   1. z_ref = (z_max + z_min)/2 (:197) for both axes staged in LDS, padded with the last row
-//      (:81-88); the bounds were loaded (16-B coalesced, whole walk in flight) into registers
-//      while the previous walk was being solved;
+// Mapping: one 64-lane wavefront per walk (both axes):
+//   1. the walk's bounds (16-B coalesced, whole walk in flight) → z_ref = (z_max + z_min)/2
+//      (:197) for both axes in LDS, padded with the last row (:81-88); the gain row k is
+//      staged in LDS next to it;
 //   2. correlation: lane l owns timesteps [l·CW, l·CW + CW), a CW-deep register sliding
-//      window, k from scalar loads (wave-uniform index): one LDS read per CW FMAs per axis;
-//   3. chunked affine scan over the 64 lanes with P = Ā^CW (Ā = A - B kxᵀ), Kogge-Stone;
+//      window, k read as a wave-uniform LDS broadcast: one z_ref read per CW FMAs per axis;
+//   3. chunked affine scan over the 64 lanes with P = Ā^CW (Ā = A - B kxᵀ, powers from the
+//      plan), Kogge-Stone;
 //   4. each lane replays its chunk in the reference form x⁺ = A x + B u with the F_ext kick
-//      (:105-106); history rows are staged in LDS and leave as contiguous 1-KiB wave stores,
-//      which drain while the next walk computes.
+//      (:105-106); history rows are staged in LDS and leave as contiguous 1-KiB wave stores.
+// Walks longer than 64·8+1 samples take several correlation passes with f kept in LDS.
 #include <algorithm>
 #include <climits>
 #include <cstdint>
@@ -85,7 +85,7 @@ struct ZrLayout {
 
 struct RolloutGeom {
   int cw, passes, kc, lz, lzp, nf;
-  int nbuf;  // z_ref buffers per wave: 2 (prefetching persistent kernel) or 1
+  int kcp;  // doubles of LDS for the staged gain row (kc rounded up to even)
 };
 
 RolloutGeom rollout_geom(int N, int64_t n) {
@@ -102,16 +102,16 @@ RolloutGeom rollout_geom(int N, int64_t n) {
   if (g.lzp < stage_min) g.lzp = (int)stage_min;
   g.lzp = (g.lzp + 1) & ~1;
   g.nf = g.passes == 1 ? 0 : (int)((nsteps + 2) & ~1LL);  // f lives in LDS only if passes > 1
-  g.nbuf = g.passes == 1 ? 2 : 1;
+  g.kcp = (g.kc + 1) & ~1;
   return g;
 }
 
 size_t lds_bytes(const RolloutGeom& g) {
-  return (size_t)(g.nbuf * 2 * g.lzp + 2 * g.nf) * sizeof(double);
+  return (size_t)(g.kcp + 2 * g.lzp + 2 * g.nf) * sizeof(double);
 }
 
 struct RolloutArgs {
-  int kc, lz, lzp, n;
+  int kc, kcp, lz, lzp, n;
   int64_t B;
   LipmConsts lc;
   const double* k;
@@ -124,6 +124,7 @@ struct RolloutArgs {
   int64_t kick_step;
   double* hist;
   int32_t* status;
+  const double* scanP;  // [8][6][9]: (Ā^C)^(2^r) for C = 1..8 (plan), or null
   int dbg;
 };
 
@@ -186,9 +187,13 @@ __device__ __forceinline__ void store_zref(const RolloutArgs& a, const BoundRegs
 }
 
 // f for lane l's CW timesteps of one pass starting at i0 (both axes).
+// k is read from the wave's LDS copy (ks): wave-uniform broadcast reads keep every lgkm
+// operation of the loop an in-order LDS access, so waits stay counted (a scalar load here
+// would force lgkmcnt(0) drains of the z_ref reads in flight).
 template <int CW>
-__device__ __forceinline__ void correlate(const RolloutArgs& a, const double* zr0,
-                                          const double* zr1, int i0, double* a0, double* a1) {
+__device__ __forceinline__ void correlate(const RolloutArgs& a, const double* ks,
+                                          const double* zr0, const double* zr1, int i0,
+                                          double* a0, double* a1) {
   using ZL = ZrLayout<CW>;
   // i0 is a multiple of CW, so idx(i0 + c) = idx(i0) + idx(c): compile-time offsets
   const double* z0 = zr0 + ZL::idx(i0);
@@ -201,7 +206,7 @@ __device__ __forceinline__ void correlate(const RolloutArgs& a, const double* zr
     w0[m] = z0[ZL::idx(1 + m)];
     w1[m] = z1[ZL::idx(1 + m)];
   }
-  const double* __restrict__ k = a.k;
+  const double* k = ks;
   for (int j = 0; j < a.kc; j += CW) {
 #pragma unroll
     for (int jj = 0; jj < CW; ++jj) {
@@ -225,7 +230,8 @@ template <int CW, bool REGF>
 __device__ __forceinline__ void scan_replay_store(const RolloutArgs& a, int64_t b, int lane,
                                                   const double* a0, const double* a1,
                                                   const double* f0, const double* f1,
-                                                  double* stage) {
+                                                  double* stage, const double* xi0,
+                                                  const double* xi1, double kk) {
   const int n = a.n, nsteps = n - 1;
   const LipmConsts lc = a.lc;
   const double kx0 = a.kx[0], kx1 = a.kx[1], kx2 = a.kx[2];
@@ -241,7 +247,6 @@ __device__ __forceinline__ void scan_replay_store(const RolloutArgs& a, int64_t 
   }
   const int C = REGF ? CW : (nsteps + 63) / 64;  // steps per lane chunk
   const int mbeg = lane * C;
-  const double kk = (a.kick != nullptr) ? a.kick[b] : 0.0;
   const int64_t kick_step = a.kick_step;
 
   // ---- 3. affine scan of x_{i+1} = Ā x_i + B f_i (+ kick) over 64 lane chunks ----------
@@ -265,11 +270,15 @@ __device__ __forceinline__ void scan_replay_store(const RolloutArgs& a, int64_t 
   } else {
     for (int m = mbeg; m < min(mbeg + C, nsteps); ++m) scan_step(m, f0[m], f1[m]);
   }
-  Mat3 P = Ab;  // P = Ā^C
-  for (int q = 1; q < C; ++q) P = matmul3(P, Ab);
-  const double* xb = a.x0 + b * 6;
-  const double xi0[3] = {xb[0], xb[1], xb[2]};
-  const double xi1[3] = {xb[3], xb[4], xb[5]};
+  Mat3 P;  // P = Ā^C (from the plan for C <= 8)
+  const bool pre = REGF && a.scanP != nullptr;
+  if (pre) {
+#pragma unroll
+    for (int q = 0; q < 9; ++q) P.m[q] = a.scanP[(C - 1) * 54 + q];
+  } else {
+    P = Ab;
+    for (int q = 1; q < C; ++q) P = matmul3(P, Ab);
+  }
   if (lane == 0) {
     double t[3];
     matvec3(P, xi0, t);
@@ -279,7 +288,8 @@ __device__ __forceinline__ void scan_replay_store(const RolloutArgs& a, int64_t 
   }
   // inclusive Kogge-Stone: T_l += P^d T_{l-d}
   Mat3 Pd = P;
-  for (int d = 1; d < ((a.dbg & 2) ? 1 : 64); d <<= 1) {
+  int r2 = 0;
+  for (int d = 1; d < ((a.dbg & 2) ? 1 : 64); d <<= 1, ++r2) {
     double u0[3], u1[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -293,7 +303,12 @@ __device__ __forceinline__ void scan_replay_store(const RolloutArgs& a, int64_t 
       matvec3(Pd, u1, t);
       for (int i = 0; i < 3; ++i) s1[i] += t[i];
     }
-    Pd = matmul3(Pd, Pd);
+    if (pre && r2 < 5) {
+#pragma unroll
+      for (int q = 0; q < 9; ++q) Pd.m[q] = a.scanP[(C - 1) * 54 + (r2 + 1) * 9 + q];
+    } else {
+      Pd = matmul3(Pd, Pd);
+    }
   }
   double x[3], y[3];
 #pragma unroll
@@ -374,39 +389,36 @@ __device__ __forceinline__ void scan_replay_store(const RolloutArgs& a, int64_t 
   }
 }
 
-// Walks of at most 64·CW+1 samples (one correlation pass): persistent over walks, f in
-// registers, the next walk's bounds in flight in registers while this walk computes,
-// z_ref double-buffered in LDS (buffer A = this walk, B = next walk; A is the staging area
-// of this walk's history once its correlation is done).
+// Walks of at most 64·CW+1 samples (one correlation pass): one wave per walk, f stays in
+// registers (lane l's CW outputs are exactly its scan chunk).
 template <int CW>
 __global__ void __launch_bounds__(64) zmpc_rollout_unc_kernel(RolloutArgs a) {
   constexpr int PF = CW + 1;  // 64·(CW+1) >= n
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int lane = threadIdx.x;
-  double* buf[2] = {smem, smem + 2 * a.lzp};
-  int cur = 0;
+  const int64_t b = blockIdx.x;
+  double* ks = smem;
+  double* zr0 = smem + a.kcp;
+  double* zr1 = zr0 + a.lzp;
   BoundRegs<PF> r;
-  int64_t b = blockIdx.x;
-  if (b < a.B && !(a.dbg & 8)) load_bounds<PF>(a, b, lane, r);
-  if (b < a.B) store_zref<CW, PF>(a, r, buf[cur], buf[cur] + a.lzp, lane);
-  for (; b < a.B; b += gridDim.x) {
-    const int64_t bn = b + gridDim.x;
-    if (bn < a.B && !(a.dbg & 8)) load_bounds<PF>(a, bn, lane, r);  // in flight meanwhile
-    __syncthreads();
-    double a0[CW], a1[CW];
-    if (!(a.dbg & 1)) {
-      correlate<CW>(a, buf[cur], buf[cur] + a.lzp, lane * CW, a0, a1);
-    } else {
+  if (!(a.dbg & 8)) load_bounds<PF>(a, b, lane, r);
+  // everything the tail needs is requested up front, behind the bound loads
+  const double* xb = a.x0 + b * 6;
+  const double xi0[3] = {xb[0], xb[1], xb[2]};
+  const double xi1[3] = {xb[3], xb[4], xb[5]};
+  const double kk = (a.kick != nullptr) ? a.kick[b] : 0.0;
+  for (int j = lane; j < a.kcp; j += 64) ks[j] = a.k[j];
+  store_zref<CW, PF>(a, r, zr0, zr1, lane);
+  __syncthreads();
+  double a0[CW], a1[CW];
+  if (!(a.dbg & 1)) {
+    correlate<CW>(a, ks, zr0, zr1, lane * CW, a0, a1);
+  } else {
 #pragma unroll
-      for (int m = 0; m < CW; ++m) a0[m] = a1[m] = 0.0;
-    }
-    // the next walk's z_ref goes to the other buffer before this walk's stores are issued
-    // (so waiting for its loads never waits for this walk's stores)
-    if (bn < a.B) store_zref<CW, PF>(a, r, buf[cur ^ 1], buf[cur ^ 1] + a.lzp, lane);
-    __syncthreads();
-    scan_replay_store<CW, true>(a, b, lane, a0, a1, nullptr, nullptr, buf[cur]);
-    cur ^= 1;
+    for (int m = 0; m < CW; ++m) a0[m] = a1[m] = 0.0;
   }
+  __syncthreads();
+  scan_replay_store<CW, true>(a, b, lane, a0, a1, nullptr, nullptr, zr0, xi0, xi1, kk);
 }
 
 // Longer walks (several correlation passes): one walk per wave, f through LDS.
@@ -418,10 +430,12 @@ __global__ void __launch_bounds__(64) zmpc_rollout_unc_long_kernel(RolloutArgs a
   const int lane = threadIdx.x;
   const int n = a.n, nsteps = n - 1;
   const int passes = (nsteps + 64 * CW - 1) / (64 * CW);
-  double* zr0 = smem;
-  double* zr1 = smem + a.lzp;
-  double* f0 = smem + 2 * a.lzp;
+  double* ks = smem;
+  double* zr0 = smem + a.kcp;
+  double* zr1 = zr0 + a.lzp;
+  double* f0 = zr1 + a.lzp;
   double* f1 = f0 + ((nsteps + 2) & ~1);
+  for (int j = lane; j < a.kcp; j += 64) ks[j] = a.k[j];
   {
     const double2* zmx = reinterpret_cast<const double2*>(a.zmax + b * a.bstride);
     const double2* zmn = reinterpret_cast<const double2*>(a.zmin + b * a.bstride);
@@ -456,7 +470,7 @@ __global__ void __launch_bounds__(64) zmpc_rollout_unc_long_kernel(RolloutArgs a
   for (int pass = 0; pass < passes; ++pass) {
     const int i0 = pass * 64 * CW + lane * CW;
     double a0[CW], a1[CW];
-    correlate<CW>(a, zr0, zr1, i0, a0, a1);
+    correlate<CW>(a, ks, zr0, zr1, i0, a0, a1);
 #pragma unroll
     for (int m = 0; m < CW; ++m) {
       if (i0 + m < nsteps) {
@@ -466,7 +480,11 @@ __global__ void __launch_bounds__(64) zmpc_rollout_unc_long_kernel(RolloutArgs a
     }
   }
   __syncthreads();
-  scan_replay_store<CW, false>(a, b, lane, nullptr, nullptr, f0, f1, smem);
+  const double* xb = a.x0 + b * 6;
+  const double xi0[3] = {xb[0], xb[1], xb[2]};
+  const double xi1[3] = {xb[3], xb[4], xb[5]};
+  const double kk = (a.kick != nullptr) ? a.kick[b] : 0.0;
+  scan_replay_store<CW, false>(a, b, lane, nullptr, nullptr, f0, f1, zr0, xi0, xi1, kk);
 }
 
 // Batched predict_wieber_axis (strict=False): one wave per instance.
@@ -502,12 +520,7 @@ int g_cus = 0;  // CUs of the device the attributes were set on (grid sizing)
 template <int CW>
 void launch_unc(const RolloutGeom& g, size_t lds, hipStream_t s, const RolloutArgs& a) {
   if (g.passes == 1) {
-    // enough waves to fill the chip (LDS admits 160 KiB / lds per CU), >= 2 walks per wave
-    // where the batch allows, so that every wave's second walk loads behind its first
-    const int per_cu = std::max<int>(1, std::min<int>(16, (int)((160 * 1024) / lds)));
-    const int64_t cap = (int64_t)std::max(g_cus, 1) * per_cu;
-    const int64_t grid = std::min<int64_t>(std::max<int64_t>((a.B + 1) / 2, 1), cap);
-    hipLaunchKernelGGL(zmpc_rollout_unc_kernel<CW>, dim3((unsigned)grid), dim3(64), lds, s, a);
+    hipLaunchKernelGGL(zmpc_rollout_unc_kernel<CW>, dim3((unsigned)a.B), dim3(64), lds, s, a);
   } else {
     hipLaunchKernelGGL(zmpc_rollout_unc_long_kernel<CW>, dim3((unsigned)a.B), dim3(64), lds, s,
                        a);
@@ -540,8 +553,9 @@ hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, con
     const char* e = getenv("ZMPC_DEBUG_ROLLOUT");  // diagnostic ablation bits (0 in production)
     return e ? atoi(e) : 0;
   }();
-  RolloutArgs a{g.kc, g.lz, g.lzp, (int)n, B,    p->lc,     p->k,   p->kx, zmax,
-                zmin, bstride, x0,  kick,   kick_step, hist, status, dbg};
+  RolloutArgs a{g.kc, g.kcp, g.lz,      g.lzp, (int)n,     B,   p->lc,
+                p->k, p->kx,  zmax,      zmin,  bstride,    x0,  kick,
+                kick_step,    hist, status, p->scanP, dbg};
   switch (g.cw) {
 #define ZMPC_CW(C)               \
   case C:                        \

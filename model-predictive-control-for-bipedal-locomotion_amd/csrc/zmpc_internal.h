@@ -30,6 +30,7 @@ struct zmpc_plan {
   double* L = nullptr;   // [N,N] lower Cholesky factor of M
   double* k = nullptr;   // [Kpad] gain row e0ᵀ M⁻¹ Puᵀ (zero-padded)
   double* kx = nullptr;  // [3]  k·Px
+  double* scanP = nullptr;  // [8][6][9] (Ā^C)^(2^r) rollout scan propagators
   double* X = nullptr;   // [N,N] L⁻¹ Puᵀ (strict plans)
   double* G = nullptr;   // [N,N] Pu (R I + Q PuᵀPu)⁻¹ Puᵀ (strict plans)
   double* v = nullptr;   // [N]   first column of Pu⁻¹ (strict plans)
