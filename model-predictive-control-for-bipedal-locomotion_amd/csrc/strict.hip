@@ -4,21 +4,24 @@
 //   min_J ½Q‖Px x + Pu J − z_ref‖² + ½R‖J‖²   s.t.  z_min ≤ Px x + Pu J ≤ z_max,  u0 = J[0]
 // Pu is lower-triangular Toeplitz with p(0) ≠ 0, hence invertible: in ZMP coordinates
 // z = Px x + Pu J the constraints are simple bounds and the problem is a strictly convex
-// box-QP, always feasible.  With c = Px x and the plan's G = Pu (R·I + Q·PuᵀPu)⁻¹ Puᵀ
-// (the inverse z-space Hessian):
-//   unconstrained     z* = c + Q·G (z_ref − c)
-//   active set A      z  = z* − G ν,   ν_A = G_AA⁻¹ (z*_A − t_A),  t = bound value
-//   KKT               ν ≥ 0 on upper-active, ν ≤ 0 on lower-active, z_min ≤ z ≤ z_max on free
-//   first jerk        u0 = (z_0 − c_0) / p(0) = (D_0 − (Gν)_0) / p(0),  D = Q·G(z_ref − c)
-// The active set is found by a primal-dual active-set iteration warm-started from the
-// previous timestep's set shifted by one horizon slot (the rollout's windows slide by one).
+// box-QP, always feasible.  With c = Px x, W = Q (z_ref − c), the plan's
+// G = Pu (R·I + Q·PuᵀPu)⁻¹ Puᵀ (inverse z-space Hessian) and H = G⁻¹ = Q I + R Pu⁻ᵀPu⁻¹,
+// everything relative to c (δ = z − c, t = bound − c):
+//   unconstrained   δ* = D = G W
+//   dual side       (|A| <= |F|)  G_AA ν_A = D_A − t_A,   δ = D − G_{:,A} ν_A
+//   primal side     (|A| >  |F|)  H_FF δ_F = W_F − H_FA t_A,  δ_A = t_A,  ν_A = W_A − (H δ)_A
+//   KKT             ν ≥ 0 on upper-active, ν ≤ 0 on lower-active, t_lo ≤ δ ≤ t_hi on free
+//   first jerk      u0 = δ_0 / p(0)
+// The active set comes from a primal-dual active-set iteration warm-started with the previous
+// timestep's set shifted one horizon slot (the rollout's windows slide by one).
 //
 // Mapping: a workgroup (4 waves) owns a tile of 16 instances (instance = walk × axis) for the
 // whole rollout, persistent over tiles.  Per timestep:
-//   GEMM   D[:, 16 instances] = G · W with W = Q (z_ref − c): v_mfma_f64_16x16x4_f64, G from
-//          L2 (batch-invariant, 176 KB at N=150), W/D tile in LDS;
-//   solve  each wave takes 4 instances: PDAS; G_AA Cholesky in LDS (in a per-wave global
-//          scratch when |A| is large), state advance, kick, history store, next W.
+//   GEMM   D[:, 16 instances] = G · W: v_mfma_f64_16x16x4_f64, G streamed from L2 (batch-
+//          invariant) with the next k-group's loads in flight under the current MFMAs;
+//   solve  each wave takes 4 instances: PDAS with the reduced Cholesky factor packed in LDS
+//          (lane-blocked 8×8 updates, LDS-only ordering), G/H row combinations as coalesced,
+//          4-row-deep pipelined loads; state advance, kick, history, next W.
 #include <cstdio>
 #include <cstdlib>
 
@@ -31,21 +34,19 @@ typedef double dbl4 __attribute__((ext_vector_type(4)));
 constexpr int SNB = 16;            // instances per tile (= MFMA column tile)
 constexpr int SWAVES = 4;          // waves per workgroup
 constexpr int SPW = SNB / SWAVES;  // instances per wave
-constexpr int SMAX_RT = 8;         // row tiles per wave (N <= 512)
 constexpr int SMAXIT = 64;         // PDAS iteration cap
 
 struct StrictArgs {
   int N, Np, ld;         // horizon, padded to 16, W/D leading dimension
-  int pcap;              // LDS doubles for the packed reduced factor
+  int pcap;              // LDS doubles for the packed reduced factor (per wave)
   int window_mode;       // 0 = rollout over [B,n,2] bounds, 1 = single step on [B,N] windows
   int64_t n;             // samples per walk (rollout)
   int64_t bstride;       // doubles between walks' bound arrays (0 = shared CoP)
   int64_t ninst;         // instances: 2B (rollout) or B (step)
-  double Q, p0;
+  double Q, p0, hg;
   LipmConsts lc;
   const double* G;       // [N,N] inverse z-space Hessian
   const double* Hz;      // [N,N] z-space Hessian Q I + R Pu⁻ᵀPu⁻¹
-  const double* Px;      // [N,3]
   const double* zmax;
   const double* zmin;
   const double* x0;      // rollout [B,2,3], step [B,3]
@@ -61,7 +62,8 @@ struct StrictArgs {
 struct PhaseClock {
   unsigned long long* dbg;
   unsigned long long t;
-  __device__ explicit PhaseClock(unsigned long long* d) : dbg(d), t(d ? __builtin_amdgcn_s_memtime() : 0) {}
+  __device__ explicit PhaseClock(unsigned long long* d)
+      : dbg(d), t(d ? __builtin_amdgcn_s_memtime() : 0) {}
   __device__ void lap(int slot, int lane) {
     if (!dbg) return;
     const unsigned long long now = __builtin_amdgcn_s_memtime();
@@ -73,8 +75,15 @@ struct PhaseClock {
   }
 };
 
+// Orders this wave's global and LDS accesses (waits for both counters).
 __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+}
+// Orders this wave's LDS accesses only: DS instructions of one wave execute in order, so a
+// compiler barrier is all a cross-lane LDS hand-off inside the wave needs.
+__device__ __forceinline__ void lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   __builtin_amdgcn_wave_barrier();
 }
 
@@ -83,6 +92,16 @@ __device__ __forceinline__ void lipm_step(const LipmConsts& c, const double* x, 
   y[0] = x[0] + c.T * x[1] + c.T2_2 * x[2] + c.T3_6 * u;
   y[1] = x[1] + c.T * x[2] + c.T2_2 * u;
   y[2] = x[2] + c.T * u;
+}
+
+// c_j = Px[j]·x with Px[j] = [1, T(j+1), T²/2 (j+1)² − h/g] evaluated as the plan (and the
+// reference, zmp_controller.py:167-169) evaluates it.
+__device__ __forceinline__ double px_dot(const StrictArgs& a, int j, const double* x) {
+#pragma clang fp contract(off)
+  const long long q = j + 1;
+  const double p1 = a.lc.T * (double)q;
+  const double p2 = a.lc.T2_2 * (double)(q * q) - a.hg;
+  return x[0] + p1 * x[1] + p2 * x[2];
 }
 
 // Window element j of instance `inst` at timestep i (rows i+1.., padded with the last row,
@@ -96,19 +115,26 @@ __device__ __forceinline__ int64_t bound_index(const StrictArgs& a, int64_t inst
   return b * a.bstride + t * 2 + axis;
 }
 
-// W[j] = Q (z_ref_j − c_j), c = Px x; zero on the padding rows.
+// W[j] = Q (z_ref_j − c_j); zero on the padding rows.
+template <int NJ>
 __device__ void build_w(const StrictArgs& a, int64_t inst, int64_t i, const double* x,
                         double* W, int lane) {
-  for (int j = lane; j < a.Np; j += 64) {
-    double w = 0.0;
+  double hi[NJ], lo[NJ];
+#pragma unroll
+  for (int c = 0; c < NJ; ++c) {
+    const int j = lane + 64 * c;
     if (j < a.N) {
       const int64_t e = bound_index(a, inst, i, j);
-      const double zr = (a.zmax[e] + a.zmin[e]) / 2;
-      const double c = a.Px[3 * j] * x[0] + a.Px[3 * j + 1] * x[1] + a.Px[3 * j + 2] * x[2];
-      w = a.Q * (zr - c);
+      hi[c] = a.zmax[e];
+      lo[c] = a.zmin[e];
     }
-    W[j] = w;
   }
+#pragma unroll
+  for (int c = 0; c < NJ; ++c) {
+    const int j = lane + 64 * c;
+    if (j < a.N) W[j] = a.Q * ((hi[c] + lo[c]) / 2 - px_dot(a, j, x));
+  }
+  for (int j = a.N + lane; j < a.Np; j += 64) W[j] = 0.0;
 }
 
 // Reduced-system factor storage: packed lower triangle in LDS (i(i+1)/2 + j) or a dense
@@ -119,6 +145,12 @@ struct Tri {
   int m;
   __device__ __forceinline__ double& at(int i, int j) const {
     return PACKED ? S[(i * (i + 1) >> 1) + j] : S[i * m + j];
+  }
+  __device__ __forceinline__ void sync() const {
+    if (PACKED)
+      lds_sync();
+    else
+      wave_sync();
   }
 };
 
@@ -135,47 +167,48 @@ __device__ bool wave_cholesky(const Tri<PACKED>& T, int lane) {
     if (!(d > 0.0)) return false;
     const double piv = sqrt(d);
     const double inv = 1.0 / piv;
-    wave_sync();
+    T.sync();
     for (int i = k + 1 + lane; i < m; i += 64) T.at(i, k) *= inv;
     if (lane == 0) T.at(k, k) = piv;
-    wave_sync();
+    T.sync();
     const int r = m - k - 1;
     const int nb = (r + 7) >> 3;
     for (int bi = 0; bi < nb; ++bi) {
       const int i = k + 1 + 8 * bi + li;
+      const double lik = (i < m) ? T.at(i, k) : 0.0;
       for (int bj = 0; bj <= bi; ++bj) {
         const int j = k + 1 + 8 * bj + lj;
-        if (i < m && j <= i) T.at(i, j) -= T.at(i, k) * T.at(j, k);
+        if (i < m && j <= i) T.at(i, j) -= lik * T.at(j, k);
       }
     }
-    wave_sync();
+    T.sync();
   }
   return true;
 }
 
-// Solve (L Lᵀ) v = rhs in place (rhs in v), L from wave_cholesky.
+// Solve (L Lᵀ) v = rhs in place (rhs in v, LDS), L from wave_cholesky.
 template <bool PACKED>
 __device__ void wave_chol_solve(const Tri<PACKED>& T, double* v, int lane) {
   const int m = T.m;
   for (int j = 0; j < m; ++j) {
     const double yj = v[j] / T.at(j, j);
-    wave_sync();
+    T.sync();
     for (int i = j + 1 + lane; i < m; i += 64) v[i] -= T.at(i, j) * yj;
     if (lane == 0) v[j] = yj;
-    wave_sync();
+    T.sync();
   }
   for (int j = m - 1; j >= 0; --j) {
     const double yj = v[j] / T.at(j, j);
-    wave_sync();
+    T.sync();
     for (int i = lane; i < j; i += 64) v[i] -= T.at(j, i) * yj;
     if (lane == 0) v[j] = yj;
-    wave_sync();
+    T.sync();
   }
 }
 
 struct WaveWork {
-  double* zs;    // [Np] unconstrained z* − c  (= D)
-  double* zz;    // [Np] current z − c
+  double* zs;    // [Np] D = unconstrained δ*
+  double* zz;    // [Np] current δ
   double* lo;    // [Np] z_min − c
   double* hi;    // [Np] z_max − c
   double* nuf;   // [Np] multipliers scattered to horizon slots
@@ -186,7 +219,65 @@ struct WaveWork {
   double* Sg;    // [N*N] global factor scratch
 };
 
-constexpr int SNJ = 8;  // horizon slots per lane (N <= 512)
+// acc[c] −= Σ_r M[idx[r]][j_c] · coef[r] for the lane's horizon slots j_c = lane + 64c:
+// one coalesced row load per (r, c); four rows in flight per round.
+template <int NJ>
+__device__ __forceinline__ void row_combine(const double* M, int N, const int* idx,
+                                            const double* coef, int count, double* acc,
+                                            int lane) {
+  int r0 = 0;
+  for (; r0 + 4 <= count; r0 += 4) {
+    double g[4][NJ];
+    double cf[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const double* row = M + (size_t)idx[r0 + u] * N;
+      cf[u] = coef[r0 + u];
+#pragma unroll
+      for (int c = 0; c < NJ; ++c) {
+        const int j = lane + 64 * c;
+        g[u][c] = (j < N) ? row[j] : 0.0;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int c = 0; c < NJ; ++c) acc[c] = fma(-g[u][c], cf[u], acc[c]);
+  }
+  for (; r0 < count; ++r0) {
+    const double* row = M + (size_t)idx[r0] * N;
+    const double cf = coef[r0];
+#pragma unroll
+    for (int c = 0; c < NJ; ++c) {
+      const int j = lane + 64 * c;
+      if (j < N) acc[c] = fma(-row[j], cf, acc[c]);
+    }
+  }
+}
+
+// Gather the reduced matrix (gather(r, c), r >= c) into the packed LDS factor, 8×8 lane
+// blocks, every load of a block row in flight before its stores.
+template <class Gather>
+__device__ __forceinline__ void gather_packed(const Tri<true>& T, Gather gather, int lane) {
+  const int m = T.m;
+  const int nb = (m + 7) >> 3;
+  const int li = lane >> 3, lj = lane & 7;
+  constexpr int kMaxNb = 16;  // m <= 128
+  for (int bi = 0; bi < nb; ++bi) {
+    const int r = 8 * bi + li;
+    double v[kMaxNb];
+#pragma unroll
+    for (int bj = 0; bj < kMaxNb; ++bj) {
+      const int c = 8 * bj + lj;
+      if (bj <= bi && r < m && c <= r) v[bj] = gather(r, c);
+    }
+#pragma unroll
+    for (int bj = 0; bj < kMaxNb; ++bj) {
+      const int c = 8 * bj + lj;
+      if (bj <= bi && r < m && c <= r) T.at(r, c) = v[bj];
+    }
+  }
+}
 
 // Factor the reduced matrix gathered by `gather(r, c)` (size m) and solve in place on w.nuc.
 template <class Gather>
@@ -194,11 +285,10 @@ __device__ bool reduced_solve(const StrictArgs& a, const WaveWork& w, int m, Gat
                               int lane) {
   PhaseClock clk(a.dbg);
   clk.count(12, m, lane);
-  if (m * (m + 1) / 2 <= a.pcap) {
+  if (m * (m + 1) / 2 <= a.pcap && m <= 128) {
     Tri<true> T{w.S, m};
-    for (int r = lane; r < m; r += 64)
-      for (int c = 0; c <= r; ++c) T.at(r, c) = gather(r, c);
-    wave_sync();
+    gather_packed(T, gather, lane);
+    lds_sync();
     clk.lap(2, lane);
     if (!wave_cholesky(T, lane)) return false;
     clk.lap(3, lane);
@@ -218,28 +308,40 @@ __device__ bool reduced_solve(const StrictArgs& a, const WaveWork& w, int m, Gat
   return true;
 }
 
-// One strict QP solve for one instance.  D holds Q·G(z_ref − c) on entry; st is the
-// instance's warm-start status array (0 free, 1 upper, 2 lower), updated in place.
-// Each primal-dual active-set iteration solves the reduced KKT system on the smaller side:
-//   dual   (|A| <= |F|):  G_AA ν_A = (z* − t)_A,            z = z* − G_{:,A} ν_A
-//   primal (|A| >  |F|):  H_FF z_F = W_F − H_FA t_A (H = G⁻¹, W = Q(z_ref − c)),
-//                         ν_A = W_A − (H z)_A
-// (all in coordinates relative to c = Px x).  Returns u0; ORs failure flags into *flags.
+// One strict QP solve for one instance.  D holds G·W on entry; st is the instance's
+// warm-start status array (0 free, 1 upper, 2 lower), updated in place.  Returns u0 and
+// ORs failure flags into *flags.
+template <int NJ>
 __device__ double solve_instance(const StrictArgs& a, int64_t inst, int64_t i, const double* x,
                                  const double* D, signed char* st, const WaveWork& w, int lane,
                                  int* flags) {
   const int N = a.N;
   PhaseClock clk(a.dbg);
-  for (int j = lane; j < N; j += 64) {
-    const int64_t e = bound_index(a, inst, i, j);
-    const double c = a.Px[3 * j] * x[0] + a.Px[3 * j + 1] * x[1] + a.Px[3 * j + 2] * x[2];
-    w.hi[j] = a.zmax[e] - c;
-    w.lo[j] = a.zmin[e] - c;
-    w.zs[j] = D[j];
-    w.zz[j] = D[j];
-    w.nuf[j] = 0.0;
+  {
+    double hi[NJ], lo[NJ];
+#pragma unroll
+    for (int c = 0; c < NJ; ++c) {
+      const int j = lane + 64 * c;
+      if (j < N) {
+        const int64_t e = bound_index(a, inst, i, j);
+        hi[c] = a.zmax[e];
+        lo[c] = a.zmin[e];
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < NJ; ++c) {
+      const int j = lane + 64 * c;
+      if (j < N) {
+        const double cj = px_dot(a, j, x);
+        w.hi[j] = hi[c] - cj;
+        w.lo[j] = lo[c] - cj;
+        w.zs[j] = D[j];
+        w.zz[j] = D[j];
+        w.nuf[j] = 0.0;
+      }
+    }
   }
-  wave_sync();
+  lds_sync();
   clk.lap(0, lane);
   clk.count(11, 1, lane);
   const double tolz = 1e-13, tolnu = 1e-13;
@@ -248,8 +350,9 @@ __device__ double solve_instance(const StrictArgs& a, int64_t inst, int64_t i, c
     clk.count(9, 1, lane);
     // compact the active and the free slots
     int m = 0, f = 0;
-    for (int j0 = 0; j0 < N; j0 += 64) {
-      const int j = j0 + lane;
+#pragma unroll
+    for (int c = 0; c < NJ; ++c) {
+      const int j = lane + 64 * c;
       const bool act = (j < N) && st[j] != 0;
       const bool fre = (j < N) && st[j] == 0;
       const unsigned long long ba = __ballot(act), bf = __ballot(fre);
@@ -259,22 +362,26 @@ __device__ double solve_instance(const StrictArgs& a, int64_t inst, int64_t i, c
       m += __popcll(ba);
       f += __popcll(bf);
     }
-    wave_sync();
+    lds_sync();
     clk.lap(1, lane);
     clk.count(10, m, lane);
     if (m > f) clk.count(13, 1, lane);
     if (m == 0) {
-      for (int j = lane; j < N; j += 64) {
-        w.zz[j] = w.zs[j];
-        w.nuf[j] = 0.0;
+#pragma unroll
+      for (int c = 0; c < NJ; ++c) {
+        const int j = lane + 64 * c;
+        if (j < N) {
+          w.zz[j] = w.zs[j];
+          w.nuf[j] = 0.0;
+        }
       }
     } else if (m <= f) {
-      // dual: G_AA ν = z*_A − t_A
+      // dual: G_AA ν = D_A − t_A
       for (int r = lane; r < m; r += 64) {
         const int j = w.ia[r];
         w.nuc[r] = w.zs[j] - (st[j] == 1 ? w.hi[j] : w.lo[j]);
       }
-      wave_sync();
+      lds_sync();
       const int* ia = w.ia;
       const double* G = a.G;
       if (!reduced_solve(a, w, m, [&](int r, int c) { return G[(size_t)ia[r] * N + ia[c]]; },
@@ -282,28 +389,44 @@ __device__ double solve_instance(const StrictArgs& a, int64_t inst, int64_t i, c
         *flags |= ZMPC_ST_FACTOR;
         break;
       }
-      for (int j = lane; j < N; j += 64) w.nuf[j] = 0.0;
-      wave_sync();
+      // δ = D − G_{:,A} ν_A   (G symmetric: row ia_r is column ia_r)
+      double acc[NJ];
+#pragma unroll
+      for (int c = 0; c < NJ; ++c) {
+        const int j = lane + 64 * c;
+        acc[c] = (j < N) ? w.zs[j] : 0.0;
+        if (j < N) w.nuf[j] = 0.0;
+      }
+      lds_sync();
       for (int r = lane; r < m; r += 64) w.nuf[w.ia[r]] = w.nuc[r];
-      // z − c = D − G_{:,A} ν_A   (G symmetric: row ia_r is column ia_r)
-      for (int j = lane; j < N; j += 64) {
-        double s = w.zs[j];
-        for (int r = 0; r < m; ++r) s -= a.G[(size_t)w.ia[r] * N + j] * w.nuc[r];
-        w.zz[j] = s;
+      row_combine<NJ>(a.G, N, w.ia, w.nuc, m, acc, lane);
+#pragma unroll
+      for (int c = 0; c < NJ; ++c) {
+        const int j = lane + 64 * c;
+        if (j < N) w.zz[j] = acc[c];
       }
     } else {
-      // primal: H_FF z_F = W_F − H_FA t_A
-      for (int j = lane; j < N; j += 64)
-        w.zz[j] = (st[j] == 1) ? w.hi[j] : ((st[j] == 2) ? w.lo[j] : 0.0);
-      wave_sync();
-      for (int r = lane; r < f; r += 64) {
-        const int j = w.iff[r];
-        const double* Hj = a.Hz + (size_t)j * N;
-        double s = a.Q * ((w.hi[j] + w.lo[j]) / 2);  // W_j = Q (z_ref − c)_j
-        for (int q = 0; q < m; ++q) s -= Hj[w.ia[q]] * w.zz[w.ia[q]];
-        w.nuc[r] = s;
+      // primal: H_FF δ_F = W_F − (H t_A)_F,  ν_A = W_A − (H δ)_A
+      double y[NJ];
+#pragma unroll
+      for (int c = 0; c < NJ; ++c) {
+        const int j = lane + 64 * c;
+        y[c] = 0.0;
+        if (j < N) w.zz[j] = (st[j] == 1) ? w.hi[j] : ((st[j] == 2) ? w.lo[j] : 0.0);
       }
-      wave_sync();
+      lds_sync();
+      for (int r = lane; r < m; r += 64) w.nuc[r] = -w.zz[w.ia[r]];
+      lds_sync();
+      row_combine<NJ>(a.Hz, N, w.ia, w.nuc, m, y, lane);  // y = H t_A (scattered)
+      // W_j − y_j for every slot, kept in nuf for now
+#pragma unroll
+      for (int c = 0; c < NJ; ++c) {
+        const int j = lane + 64 * c;
+        if (j < N) w.nuf[j] = a.Q * ((w.hi[j] + w.lo[j]) / 2) - y[c];
+      }
+      lds_sync();
+      for (int r = lane; r < f; r += 64) w.nuc[r] = w.nuf[w.iff[r]];
+      lds_sync();
       const int* iff = w.iff;
       const double* H = a.Hz;
       if (f > 0 &&
@@ -313,26 +436,27 @@ __device__ double solve_instance(const StrictArgs& a, int64_t inst, int64_t i, c
         break;
       }
       for (int r = lane; r < f; r += 64) w.zz[w.iff[r]] = w.nuc[r];
-      wave_sync();
-      // ν = W − H z on the active slots, 0 on the free ones
-      for (int j = lane; j < N; j += 64) w.nuf[j] = 0.0;
-      wave_sync();
-      for (int q = lane; q < m; q += 64) {
-        const int j = w.ia[q];
-        const double* Hj = a.Hz + (size_t)j * N;
-        double s = a.Q * ((w.hi[j] + w.lo[j]) / 2);
-        for (int t = 0; t < N; ++t) s -= Hj[t] * w.zz[t];
-        w.nuf[j] = s;
+      // ν_A = (W − H t_A)_A − (H_{:,F} δ_F)_A ; 0 on the free slots
+      double v2[NJ];
+#pragma unroll
+      for (int c = 0; c < NJ; ++c) v2[c] = 0.0;
+      for (int r = lane; r < f; r += 64) w.nuc[r] = -w.nuc[r];
+      lds_sync();
+      row_combine<NJ>(a.Hz, N, w.iff, w.nuc, f, v2, lane);
+#pragma unroll
+      for (int c = 0; c < NJ; ++c) {
+        const int j = lane + 64 * c;
+        if (j < N) w.nuf[j] = (st[j] != 0) ? (w.nuf[j] - v2[c]) : 0.0;
       }
     }
-    wave_sync();
+    lds_sync();
     clk.lap(5, lane);
     // primal-dual set update: release active slots with wrong-signed multipliers, activate
     // violated free slots
-    signed char ns[SNJ];
+    signed char ns[NJ];
     bool changed = false;
 #pragma unroll
-    for (int c = 0; c < SNJ; ++c) {
+    for (int c = 0; c < NJ; ++c) {
       const int j = lane + 64 * c;
       ns[c] = 0;
       if (j < N) {
@@ -358,18 +482,69 @@ __device__ double solve_instance(const StrictArgs& a, int64_t inst, int64_t i, c
       break;
     }
 #pragma unroll
-    for (int c = 0; c < SNJ; ++c) {
+    for (int c = 0; c < NJ; ++c) {
       const int j = lane + 64 * c;
       if (j < N) st[j] = ns[c];
     }
-    wave_sync();
+    lds_sync();
   }
   if (!done) *flags |= ZMPC_ST_MAXITER;
   const double u0 = w.zz[0] / a.p0;
-  wave_sync();
+  lds_sync();
   return u0;
 }
 
+// D[:, 16 instances] = M · Win for the row tiles rt = wave + 4t (t < NJ) of one wave;
+// results returned in acc (MFMA D layout: col = lane&15, row = (lane>>4) + 4q).
+// The next k-group's M loads are issued before the current group's MFMAs.
+template <int NJ>
+__device__ __forceinline__ void tile_gemm(const double* __restrict__ M, int N, int Np,
+                                          const double* Win, int ld, int wave, int lane,
+                                          dbl4* acc) {
+  const int r = lane & 15, kq = lane >> 4;
+  const int nrt = Np >> 4;
+  const double* rows[NJ];
+  bool ok[NJ];
+#pragma unroll
+  for (int t = 0; t < NJ; ++t) {
+    acc[t] = dbl4{0.0, 0.0, 0.0, 0.0};
+    const int rt = wave + SWAVES * t;
+    const int row = rt * 16 + r;
+    ok[t] = (rt < nrt) && (row < N);
+    rows[t] = M + (ok[t] ? row : 0);
+  }
+  double gc[NJ][4], gn[NJ][4];
+  auto load_group = [&](int k0, double (&g)[NJ][4]) {
+#pragma unroll
+    for (int t = 0; t < NJ; ++t)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = k0 + 4 * u + kq;
+        g[t][u] = (ok[t] && k < N) ? rows[t][(size_t)k * N] : 0.0;
+      }
+  };
+  load_group(0, gc);
+  for (int k0 = 0; k0 < Np; k0 += 16) {
+    if (k0 + 16 < Np) load_group(k0 + 16, gn);
+    double wv[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) wv[u] = Win[r * ld + k0 + 4 * u + kq];
+#pragma unroll
+    for (int t = 0; t < NJ; ++t) {
+      if (wave + SWAVES * t < nrt) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(gc[t][u], wv[u], acc[t], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < NJ; ++t)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) gc[t][u] = gn[t][u];
+  }
+}
+
+template <int NJ>
 __global__ void __launch_bounds__(256) zmpc_strict_kernel(StrictArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -414,47 +589,23 @@ __global__ void __launch_bounds__(256) zmpc_strict_kernel(StrictArgs a) {
         // hist[b, 0, axis, :] = x0
         a.out[((inst >> 1) * a.n * 2 + (inst & 1)) * 3 + lane] = x[lane];
       }
-      if (inst < a.ninst)
-        build_w(a, inst, 0, x, Wt + s * ld, lane);
-      else
+      if (inst < a.ninst) {
+        const double xv[3] = {x[0], x[1], x[2]};
+        build_w<NJ>(a, inst, 0, xv, Wt + s * ld, lane);
+      } else {
         for (int j = lane; j < ld; j += 64) Wt[s * ld + j] = 0.0;
+      }
     }
     __syncthreads();
 
     for (int64_t i = 0; i < nsteps; ++i) {
       PhaseClock kclk(a.dbg);
       // ---- GEMM: D = G · W for the 16 instances of the tile (MFMA f64) ----------------
-      dbl4 acc[SMAX_RT];
-#pragma unroll
-      for (int t = 0; t < SMAX_RT; ++t) acc[t] = dbl4{0.0, 0.0, 0.0, 0.0};
-      {
-        const int r = lane & 15, kq = lane >> 4;
-#pragma unroll
-        for (int t = 0; t < SMAX_RT; ++t) {
-          const int rt = wave + SWAVES * t;
-          if (rt < nrt) {
-            const int row = rt * 16 + r;
-            const double* Gr = a.G + row;
-            const bool rok = row < a.N;
-            // Np is a multiple of 16: four k-steps per group, loads issued before the MFMAs
-            for (int k0 = 0; k0 < Np; k0 += 16) {
-              double gv[4], wv[4];
-#pragma unroll
-              for (int u = 0; u < 4; ++u) {
-                const int k = k0 + 4 * u + kq;
-                gv[u] = (rok && k < a.N) ? Gr[(size_t)k * a.N] : 0.0;
-                wv[u] = Wt[r * ld + k];
-              }
-#pragma unroll
-              for (int u = 0; u < 4; ++u)
-                acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(gv[u], wv[u], acc[t], 0, 0, 0);
-            }
-          }
-        }
-      }
+      dbl4 acc[NJ];
+      tile_gemm<NJ>(a.G, a.N, Np, Wt, ld, wave, lane, acc);
       __syncthreads();
 #pragma unroll
-      for (int t = 0; t < SMAX_RT; ++t) {
+      for (int t = 0; t < NJ; ++t) {
         const int rt = wave + SWAVES * t;
         if (rt < nrt) {
           const int col = lane & 15;
@@ -463,8 +614,8 @@ __global__ void __launch_bounds__(256) zmpc_strict_kernel(StrictArgs a) {
         }
       }
       __syncthreads();
-
       kclk.lap(7, lane);
+
       // ---- per-instance active set, state advance, next W ------------------------------
       for (int q = 0; q < SPW; ++q) {
         const int s = wave * SPW + q;
@@ -475,35 +626,35 @@ __global__ void __launch_bounds__(256) zmpc_strict_kernel(StrictArgs a) {
         const double xv[3] = {x[0], x[1], x[2]};
         // warm start: shift the previous set one slot towards the present
         if (i > 0) {
-          signed char v[SNJ];
+          signed char v[NJ];
 #pragma unroll
-          for (int c = 0; c < SNJ; ++c) {
+          for (int c = 0; c < NJ; ++c) {
             const int j = lane + 64 * c;
             v[c] = (j + 1 < a.N) ? st[j + 1] : ((j < a.N) ? st[j] : 0);
           }
-          wave_sync();
+          lds_sync();
 #pragma unroll
-          for (int c = 0; c < SNJ; ++c)
+          for (int c = 0; c < NJ; ++c)
             if (lane + 64 * c < a.N) st[lane + 64 * c] = v[c];
-          wave_sync();
+          lds_sync();
         }
         int fq = 0;
-        const double u0 = solve_instance(a, inst, i, xv, Wt + s * ld, st, w, lane, &fq);
+        const double u0 = solve_instance<NJ>(a, inst, i, xv, Wt + s * ld, st, w, lane, &fq);
         double xn[3];
         lipm_step(a.lc, xv, u0, xn);
         if (!a.window_mode && (inst & 1) && i == a.kick_step && a.kick != nullptr)
           xn[1] -= a.kick[inst >> 1];
         if (!(isfinite(xn[0]) && isfinite(xn[1]) && isfinite(xn[2]))) fq |= ZMPC_ST_NONFINITE;
         if (lane == 0) fl[s] |= fq;
-        wave_sync();
+        lds_sync();
         if (lane < 3) x[lane] = xn[lane];
         if (a.window_mode) {
           if (lane < 3) a.out[inst * 3 + lane] = xn[lane];
         } else if (lane < 3) {
           a.out[(((inst >> 1) * a.n + i + 1) * 2 + (inst & 1)) * 3 + lane] = xn[lane];
         }
-        wave_sync();
-        if (i + 1 < nsteps) build_w(a, inst, i + 1, xn, Wt + s * ld, lane);
+        lds_sync();
+        if (i + 1 < nsteps) build_w<NJ>(a, inst, i + 1, xn, Wt + s * ld, lane);
       }
       kclk.lap(8, lane);
       __syncthreads();
@@ -534,14 +685,21 @@ size_t strict_lds_bytes(int Np, int ld, int pcap) {
 }  // namespace
 
 hipError_t zmpc_strict_set_attrs() {
-  return hipFuncSetAttribute((const void*)zmpc_strict_kernel,
-                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  hipError_t e = hipSuccess;
+#define ZMPC_SATTR(J)                                                                   \
+  if (e == hipSuccess)                                                                  \
+    e = hipFuncSetAttribute((const void*)zmpc_strict_kernel<J>,                        \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  ZMPC_SATTR(1) ZMPC_SATTR(2) ZMPC_SATTR(3) ZMPC_SATTR(4) ZMPC_SATTR(5) ZMPC_SATTR(6)
+  ZMPC_SATTR(7) ZMPC_SATTR(8)
+#undef ZMPC_SATTR
+  return e;
 }
 
 static hipError_t launch_strict(const zmpc_plan* p, StrictArgs a, hipStream_t s,
                                 std::string* why) {
-  if (p->N > 16 * SWAVES * SMAX_RT) {
-    *why = "strict solver supports horizon N <= " + std::to_string(16 * SWAVES * SMAX_RT);
+  if (p->N > 512) {
+    *why = "strict solver supports horizon N <= 512";
     return hipErrorInvalidValue;
   }
   a.N = p->N;
@@ -560,10 +718,10 @@ static hipError_t launch_strict(const zmpc_plan* p, StrictArgs a, hipStream_t s,
   if (pcap > fit) pcap = fit;
   a.pcap = pcap & ~1;
   a.Q = p->Q;
+  a.hg = p->hg;
   a.lc = p->lc;
   a.G = p->G;
   a.Hz = p->Hz;
-  a.Px = p->Px;
   // p(0) = T³/6·1 − T h/g  (zmp_controller.py:171 with i = j)
   a.p0 = p->T3_6 - p->Thg;
   const int64_t ntiles = (a.ninst + SNB - 1) / SNB;
@@ -577,7 +735,19 @@ static hipError_t launch_strict(const zmpc_plan* p, StrictArgs a, hipStream_t s,
     (void)hipMemsetAsync(dbgbuf, 0, 32 * sizeof(unsigned long long), s);
     a.dbg = dbgbuf;
   }
-  hipLaunchKernelGGL(zmpc_strict_kernel, dim3(grid), dim3(256), lds, s, a);
+  const int nj = (a.N + 63) / 64;
+  switch (nj) {
+#define ZMPC_SCASE(J)                                                                        \
+  case J:                                                                                    \
+    hipLaunchKernelGGL(zmpc_strict_kernel<J>, dim3(grid), dim3(256), lds, s, a);             \
+    break;
+    ZMPC_SCASE(1) ZMPC_SCASE(2) ZMPC_SCASE(3) ZMPC_SCASE(4) ZMPC_SCASE(5) ZMPC_SCASE(6)
+    ZMPC_SCASE(7) ZMPC_SCASE(8)
+#undef ZMPC_SCASE
+    default:
+      *why = "unsupported horizon";
+      return hipErrorInvalidValue;
+  }
   hipError_t e = hipGetLastError();
   if (dbg_on && dbgbuf && e == hipSuccess) {
     unsigned long long h[32];
@@ -585,7 +755,7 @@ static hipError_t launch_strict(const zmpc_plan* p, StrictArgs a, hipStream_t s,
     (void)hipMemcpy(h, dbgbuf, sizeof(h), hipMemcpyDeviceToHost);
     fprintf(stderr,
             "[zmpc strict dbg] grid=%d pcap=%d cycles: prep=%llu compact=%llu gather=%llu "
-            "chol=%llu cholsolve=%llu zupd=%llu setupd=%llu gemm=%llu inst_rest=%llu "
+            "chol=%llu cholsolve=%llu branch=%llu setupd=%llu gemm=%llu inst_all=%llu "
             "barrier=%llu | solves=%llu iters=%llu sum_m=%llu primal=%llu sum_fact=%llu "
             "global_fact=%llu\n",
             grid, a.pcap, h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[15], h[11],
@@ -596,9 +766,9 @@ static hipError_t launch_strict(const zmpc_plan* p, StrictArgs a, hipStream_t s,
 
 hipError_t zmpc_launch_rollout_strict(const zmpc_plan* p, int64_t B, int64_t n,
                                       const double* zmax, const double* zmin, int64_t bstride,
-                                      const double* x0,
-                                      const double* kick, int64_t kick_step, double* hist,
-                                      int32_t* status, hipStream_t s, std::string* why) {
+                                      const double* x0, const double* kick, int64_t kick_step,
+                                      double* hist, int32_t* status, hipStream_t s,
+                                      std::string* why) {
   if (!p->G) {
     *why = "plan was created without strict workspace";
     return hipErrorInvalidValue;
