@@ -421,6 +421,191 @@ __global__ void __launch_bounds__(64) zmpc_rollout_unc_kernel(RolloutArgs a) {
   scan_replay_store<CW, true>(a, b, lane, a0, a1, nullptr, nullptr, zr0, xi0, xi1, kk);
 }
 
+// Split-axis variant of the single-pass kernel: a 128-thread workgroup per walk, wave 0
+// solves the x axis and wave 1 the y axis (half the registers and twice the waves of the
+// one-wave kernel, for latency hiding); they share the staged z_ref, gain row and history
+// staging buffer, so loads and stores stay whole-walk coalesced.
+template <int CW>
+__global__ void __launch_bounds__(128, 8) zmpc_rollout_unc_axis_kernel(RolloutArgs a) {
+  using ZL = ZrLayout<CW>;
+  constexpr int PF2 = (CW + 2) / 2;  // 128·PF2 >= 64·(CW+1) >= n
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  __shared__ int flag[2];
+  const int tid = threadIdx.x, axis = tid >> 6, lane = tid & 63;
+  const int64_t b = blockIdx.x;
+  const int n = a.n, nsteps = n - 1;
+  double* ks = smem;
+  double* zr0 = smem + a.kcp;
+  double* zr1 = zr0 + a.lzp;
+  // ---- 1. bounds → z_ref (both waves, 128 samples per round), gain row → LDS ------------
+  {
+    const double2* zmx = reinterpret_cast<const double2*>(a.zmax + b * a.bstride);
+    const double2* zmn = reinterpret_cast<const double2*>(a.zmin + b * a.bstride);
+    double2 hi[PF2], lo[PF2];
+#pragma unroll
+    for (int u = 0; u < PF2; ++u) {
+      const int t = u * 128 + tid;
+      if (t < n && !(a.dbg & 8)) {
+        hi[u] = zmx[t];
+        lo[u] = zmn[t];
+      } else {
+        hi[u] = lo[u] = make_double2(0.0, 0.0);
+      }
+    }
+    for (int j = tid; j < a.kcp; j += 128) ks[j] = a.k[j];
+#pragma unroll
+    for (int u = 0; u < PF2; ++u) {
+      const int t = u * 128 + tid;
+      if (t < n) {
+        zr0[ZL::idx(t)] = (hi[u].x + lo[u].x) / 2;
+        zr1[ZL::idx(t)] = (hi[u].y + lo[u].y) / 2;
+      }
+    }
+    const double2 h = zmx[n - 1], l = zmn[n - 1];
+    const double last0 = (h.x + l.x) / 2, last1 = (h.y + l.y) / 2;
+    for (int t = n + tid; t < a.lz; t += 128) {
+      zr0[ZL::idx(t)] = last0;
+      zr1[ZL::idx(t)] = last1;
+    }
+  }
+  const double* xb = a.x0 + b * 6 + 3 * axis;
+  const double xi[3] = {xb[0], xb[1], xb[2]};
+  const double kk = (axis == 1 && a.kick != nullptr) ? a.kick[b] : 0.0;
+  const int64_t kick_step = (axis == 1) ? a.kick_step : -1;
+  __syncthreads();
+
+  // ---- 2. correlation for this wave's axis --------------------------------------------
+  double f[CW];
+  {
+    const double* z = (axis ? zr1 : zr0) + ZL::idx(lane * CW);
+    double w[CW];
+#pragma unroll
+    for (int m = 0; m < CW; ++m) {
+      f[m] = 0.0;
+      w[m] = z[ZL::idx(1 + m)];
+    }
+    for (int j = 0; j < ((a.dbg & 1) ? 0 : a.kc); j += CW) {
+#pragma unroll
+      for (int jj = 0; jj < CW; ++jj) {
+        const double kj = ks[j + jj];
+#pragma unroll
+        for (int m = 0; m < CW; ++m) f[m] = fma(kj, w[(jj + m) % CW], f[m]);
+        w[jj] = z[ZL::idx(1 + jj + CW)];
+      }
+      z += CW + ZL::kPad;
+    }
+  }
+  __syncthreads();  // z_ref is dead from here on: the area becomes the history staging
+
+  // ---- 3. lane-chunk affine scan (this axis) -----------------------------------------
+  const LipmConsts lc = a.lc;
+  const double kx0 = a.kx[0], kx1 = a.kx[1], kx2 = a.kx[2];
+  const double Bv[3] = {lc.T3_6, lc.T2_2, lc.T};
+  Mat3 Ab;
+  {
+    const double A[9] = {1.0, lc.T, lc.T2_2, 0.0, 1.0, lc.T, 0.0, 0.0, 1.0};
+    const double kx[3] = {kx0, kx1, kx2};
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) Ab.m[3 * i + j] = A[3 * i + j] - Bv[i] * kx[j];
+  }
+  const int mbeg = lane * CW;
+  double sv[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+  for (int q = 0; q < CW; ++q) {
+    if (mbeg + q < nsteps) {
+      double t[3];
+      matvec3(Ab, sv, t);
+      sv[0] = fma(Bv[0], f[q], t[0]);
+      sv[1] = fma(Bv[1], f[q], t[1]);
+      sv[2] = fma(Bv[2], f[q], t[2]);
+      if (mbeg + q == kick_step) sv[1] -= kk;
+    }
+  }
+  const double* Pp = a.scanP + (CW - 1) * 54;  // (Ā^CW)^(2^r), r = 0..5, from the plan
+  if (lane == 0) {
+    double t[3];
+    Mat3 P;
+#pragma unroll
+    for (int q = 0; q < 9; ++q) P.m[q] = Pp[q];
+    matvec3(P, xi, t);
+    for (int i = 0; i < 3; ++i) sv[i] += t[i];
+  }
+#pragma unroll
+  for (int r2 = 0; r2 < 6; ++r2) {
+    const int d = 1 << r2;
+    if (a.dbg & 2) break;
+    double u[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) u[i] = __shfl_up(sv[i], d, 64);
+    if (lane >= d) {
+      Mat3 Pd;
+#pragma unroll
+      for (int q = 0; q < 9; ++q) Pd.m[q] = Pp[r2 * 9 + q];
+      double t[3];
+      matvec3(Pd, u, t);
+      for (int i = 0; i < 3; ++i) sv[i] += t[i];
+    }
+  }
+  double xs0[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const double p = __shfl_up(sv[i], 1, 64);
+    xs0[i] = (lane == 0) ? xi[i] : p;
+  }
+
+  // ---- 4. replay (reference form) into the shared staging rows, coalesced copy-out ----
+  double* stage = zr0;
+  const int rows_per_round = (2 * a.lzp) / 6;
+  double* hb = a.hist + b * (int64_t)n * 6;
+  double x[3];
+  for (int r0 = 0; r0 < n; r0 += rows_per_round) {
+    const int r1 = min(r0 + rows_per_round, n);
+    if (lane == 0 && r0 == 0) {
+      stage[3 * axis + 0] = xi[0];
+      stage[3 * axis + 1] = xi[1];
+      stage[3 * axis + 2] = xi[2];
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) x[i] = xs0[i];
+#pragma unroll
+    for (int q = 0; q < CW; ++q) {
+      const int m = mbeg + q;
+      if (m < nsteps) {
+        const double u = f[q] - (kx0 * x[0] + kx1 * x[1] + kx2 * x[2]);
+        double xn[3];
+        lipm_step(lc, x, u, xn);
+        if (m == kick_step) xn[1] -= kk;
+        const int row = m + 1;
+        if (row >= r0 && row < r1) {
+          double* o = stage + (row - r0) * 6 + 3 * axis;
+          o[0] = xn[0];
+          o[1] = xn[1];
+          o[2] = xn[2];
+        }
+#pragma unroll
+        for (int i = 0; i < 3; ++i) x[i] = xn[i];
+      }
+    }
+    __syncthreads();
+    if (!(a.dbg & 4)) {
+      const int nd2 = (r1 - r0) * 3;
+      const double2* src = reinterpret_cast<const double2*>(stage);
+      double2* dst = reinterpret_cast<double2*>(hb + (int64_t)r0 * 6);
+      for (int e = tid; e < nd2; e += 128) dst[e] = src[e];
+    }
+    __syncthreads();
+  }
+  if (a.status != nullptr) {
+    const bool finite = isfinite(x[0]) && isfinite(x[1]) && isfinite(x[2]);
+    const unsigned long long bad = __ballot(!finite);
+    if (lane == 0) flag[axis] = bad ? ZMPC_ST_NONFINITE : 0;
+    __syncthreads();
+    if (tid == 0) a.status[b] = flag[0] | flag[1];
+  }
+}
+
 // Longer walks (several correlation passes): one walk per wave, f through LDS.
 template <int CW>
 __global__ void __launch_bounds__(64) zmpc_rollout_unc_long_kernel(RolloutArgs a) {
@@ -519,7 +704,14 @@ int g_cus = 0;  // CUs of the device the attributes were set on (grid sizing)
 
 template <int CW>
 void launch_unc(const RolloutGeom& g, size_t lds, hipStream_t s, const RolloutArgs& a) {
-  if (g.passes == 1) {
+  static const bool one_wave = [] {
+    const char* e = getenv("ZMPC_ROLLOUT_ONEWAVE");  // diagnostic A/B: one wave per walk
+    return e != nullptr && atoi(e) != 0;
+  }();
+  if (g.passes == 1 && !one_wave) {
+    hipLaunchKernelGGL(zmpc_rollout_unc_axis_kernel<CW>, dim3((unsigned)a.B), dim3(128), lds, s,
+                       a);
+  } else if (g.passes == 1) {
     hipLaunchKernelGGL(zmpc_rollout_unc_kernel<CW>, dim3((unsigned)a.B), dim3(64), lds, s, a);
   } else {
     hipLaunchKernelGGL(zmpc_rollout_unc_long_kernel<CW>, dim3((unsigned)a.B), dim3(64), lds, s,
@@ -589,6 +781,9 @@ hipError_t zmpc_rollout_unc_set_attrs() {
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);       \
   if (e == hipSuccess)                                                                      \
     e = hipFuncSetAttribute((const void*)zmpc_rollout_unc_long_kernel<C>,                  \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);       \
+  if (e == hipSuccess)                                                                      \
+    e = hipFuncSetAttribute((const void*)zmpc_rollout_unc_axis_kernel<C>,                  \
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   ZMPC_ATTR(1) ZMPC_ATTR(2) ZMPC_ATTR(3) ZMPC_ATTR(4) ZMPC_ATTR(5) ZMPC_ATTR(6) ZMPC_ATTR(7)
   ZMPC_ATTR(8)
