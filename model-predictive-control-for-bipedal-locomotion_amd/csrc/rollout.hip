@@ -708,7 +708,8 @@ void launch_unc(const RolloutGeom& g, size_t lds, hipStream_t s, const RolloutAr
     const char* e = getenv("ZMPC_ROLLOUT_ONEWAVE");  // diagnostic A/B: one wave per walk
     return e != nullptr && atoi(e) != 0;
   }();
-  if (g.passes == 1 && !one_wave) {
+  // the split-axis kernel is built for 8 waves/SIMD: it keeps the default 64 KiB LDS cap
+  if (g.passes == 1 && !one_wave && lds <= 64 * 1024) {
     hipLaunchKernelGGL(zmpc_rollout_unc_axis_kernel<CW>, dim3((unsigned)a.B), dim3(128), lds, s,
                        a);
   } else if (g.passes == 1) {
@@ -769,7 +770,8 @@ hipError_t zmpc_launch_step_unc(const zmpc_plan* p, int64_t B, const double* x,
   return hipGetLastError();
 }
 
-// The dynamic-LDS ceiling must be raised once per device for > 64 KiB requests.
+// The dynamic-LDS ceiling must be raised once per device for > 64 KiB requests (not for the
+// split-axis kernel, whose 8-waves-per-SIMD bound caps its LDS below that).
 hipError_t zmpc_rollout_unc_set_attrs() {
   int dev = 0;
   hipError_t e = hipGetDevice(&dev);
@@ -781,9 +783,6 @@ hipError_t zmpc_rollout_unc_set_attrs() {
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);       \
   if (e == hipSuccess)                                                                      \
     e = hipFuncSetAttribute((const void*)zmpc_rollout_unc_long_kernel<C>,                  \
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);       \
-  if (e == hipSuccess)                                                                      \
-    e = hipFuncSetAttribute((const void*)zmpc_rollout_unc_axis_kernel<C>,                  \
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   ZMPC_ATTR(1) ZMPC_ATTR(2) ZMPC_ATTR(3) ZMPC_ATTR(4) ZMPC_ATTR(5) ZMPC_ATTR(6) ZMPC_ATTR(7)
   ZMPC_ATTR(8)
