@@ -97,8 +97,8 @@ RolloutGeom rollout_geom(int N, int64_t n) {
   g.lz = g.passes * 64 * g.cw + g.kc + 1;         // z_ref samples staged (padded with last)
   const int pad = (g.cw % 2 == 0) ? 1 : 0;
   g.lzp = g.lz + pad * (g.lz / g.cw) + 1;         // LDS doubles per axis
-  // the z_ref area doubles as the history staging buffer: at least half a walk of rows
-  const int64_t stage_min = ((n + 1) / 2 * 6 + 1) / 2;
+  // the z_ref area doubles as the history staging buffer: at least a third of a walk of rows
+  const int64_t stage_min = ((n + 2) / 3 * 6 + 1) / 2;
   if (g.lzp < stage_min) g.lzp = (int)stage_min;
   g.lzp = (g.lzp + 1) & ~1;
   g.nf = g.passes == 1 ? 0 : (int)((nsteps + 2) & ~1LL);  // f lives in LDS only if passes > 1
@@ -434,10 +434,12 @@ __global__ void __launch_bounds__(128, 8) zmpc_rollout_unc_axis_kernel(RolloutAr
   const int tid = threadIdx.x, axis = tid >> 6, lane = tid & 63;
   const int64_t b = blockIdx.x;
   const int n = a.n, nsteps = n - 1;
-  double* ks = smem;
-  double* zr0 = smem + a.kcp;
+  // k stays in global memory (wave-uniform scalar loads): at 8 waves per SIMD the scalar
+  // waits hide, and the LDS it would take keeps 16 walks per CU resident
+  const double* __restrict__ ks = a.k;
+  double* zr0 = smem;
   double* zr1 = zr0 + a.lzp;
-  // ---- 1. bounds → z_ref (both waves, 128 samples per round), gain row → LDS ------------
+  // ---- 1. bounds → z_ref (both waves, 128 samples per round) ---------------------------
   {
     const double2* zmx = reinterpret_cast<const double2*>(a.zmax + b * a.bstride);
     const double2* zmn = reinterpret_cast<const double2*>(a.zmin + b * a.bstride);
@@ -452,7 +454,6 @@ __global__ void __launch_bounds__(128, 8) zmpc_rollout_unc_axis_kernel(RolloutAr
         hi[u] = lo[u] = make_double2(0.0, 0.0);
       }
     }
-    for (int j = tid; j < a.kcp; j += 128) ks[j] = a.k[j];
 #pragma unroll
     for (int u = 0; u < PF2; ++u) {
       const int t = u * 128 + tid;
@@ -468,10 +469,6 @@ __global__ void __launch_bounds__(128, 8) zmpc_rollout_unc_axis_kernel(RolloutAr
       zr1[ZL::idx(t)] = last1;
     }
   }
-  const double* xb = a.x0 + b * 6 + 3 * axis;
-  const double xi[3] = {xb[0], xb[1], xb[2]};
-  const double kk = (axis == 1 && a.kick != nullptr) ? a.kick[b] : 0.0;
-  const int64_t kick_step = (axis == 1) ? a.kick_step : -1;
   __syncthreads();
 
   // ---- 2. correlation for this wave's axis --------------------------------------------
@@ -496,6 +493,10 @@ __global__ void __launch_bounds__(128, 8) zmpc_rollout_unc_axis_kernel(RolloutAr
     }
   }
   __syncthreads();  // z_ref is dead from here on: the area becomes the history staging
+  const double* xb = a.x0 + b * 6 + 3 * axis;
+  const double xi[3] = {xb[0], xb[1], xb[2]};
+  const double kk = (axis == 1 && a.kick != nullptr) ? a.kick[b] : 0.0;
+  const int64_t kick_step = (axis == 1) ? a.kick_step : -1;
 
   // ---- 3. lane-chunk affine scan (this axis) -----------------------------------------
   const LipmConsts lc = a.lc;
@@ -709,9 +710,10 @@ void launch_unc(const RolloutGeom& g, size_t lds, hipStream_t s, const RolloutAr
     return e != nullptr && atoi(e) != 0;
   }();
   // the split-axis kernel is built for 8 waves/SIMD: it keeps the default 64 KiB LDS cap
-  if (g.passes == 1 && !one_wave && lds <= 64 * 1024) {
-    hipLaunchKernelGGL(zmpc_rollout_unc_axis_kernel<CW>, dim3((unsigned)a.B), dim3(128), lds, s,
-                       a);
+  const size_t lds_axis = lds - (size_t)a.kcp * sizeof(double);  // no staged gain row
+  if (g.passes == 1 && !one_wave && lds_axis <= 64 * 1024) {
+    hipLaunchKernelGGL(zmpc_rollout_unc_axis_kernel<CW>, dim3((unsigned)a.B), dim3(128), lds_axis,
+                       s, a);
   } else if (g.passes == 1) {
     hipLaunchKernelGGL(zmpc_rollout_unc_kernel<CW>, dim3((unsigned)a.B), dim3(64), lds, s, a);
   } else {
