@@ -213,8 +213,8 @@ __global__ void zmpc_scan_matrices(double T, double T2_2, double T3_6,
     }
     double Q[9];
     for (int q = 0; q < 9; ++q) Q[q] = P[q];
-    for (int r = 0; r < 6; ++r) {
-      for (int q = 0; q < 9; ++q) out[(C - 1) * 54 + r * 9 + q] = Q[q];
+    for (int r = 0; r < kScanLevels; ++r) {
+      for (int q = 0; q < 9; ++q) out[(C - 1) * kScanStride + r * 9 + q] = Q[q];
       double t[9];
       mul(Q, Q, t);
       for (int q = 0; q < 9; ++q) Q[q] = t[q];

@@ -124,9 +124,11 @@ struct RolloutArgs {
   int64_t kick_step;
   double* hist;
   int32_t* status;
-  const double* scanP;  // [8][6][9]: (Ā^C)^(2^r) for C = 1..8 (plan), or null
+  const double* scanP;  // [8][kScanLevels][9]: (Ā^C)^(2^r) for C = 1..8 (plan), or null
   int dbg;
+  int srows;  // history rows the split-axis kernels stage per copy-out round
 };
+
 
 // Bounds of one walk held in registers: PF rounds of 64 samples, one 16-B (x, y) pair of
 // each bound array per lane and round.
@@ -274,7 +276,7 @@ __device__ __forceinline__ void scan_replay_store(const RolloutArgs& a, int64_t 
   const bool pre = REGF && a.scanP != nullptr;
   if (pre) {
 #pragma unroll
-    for (int q = 0; q < 9; ++q) P.m[q] = a.scanP[(C - 1) * 54 + q];
+    for (int q = 0; q < 9; ++q) P.m[q] = a.scanP[(C - 1) * kScanStride + q];
   } else {
     P = Ab;
     for (int q = 1; q < C; ++q) P = matmul3(P, Ab);
@@ -305,7 +307,7 @@ __device__ __forceinline__ void scan_replay_store(const RolloutArgs& a, int64_t 
     }
     if (pre && r2 < 5) {
 #pragma unroll
-      for (int q = 0; q < 9; ++q) Pd.m[q] = a.scanP[(C - 1) * 54 + (r2 + 1) * 9 + q];
+      for (int q = 0; q < 9; ++q) Pd.m[q] = a.scanP[(C - 1) * kScanStride + (r2 + 1) * 9 + q];
     } else {
       Pd = matmul3(Pd, Pd);
     }
@@ -421,84 +423,99 @@ __global__ void __launch_bounds__(64) zmpc_rollout_unc_kernel(RolloutArgs a) {
   scan_replay_store<CW, true>(a, b, lane, a0, a1, nullptr, nullptr, zr0, xi0, xi1, kk);
 }
 
-// Split-axis variant of the single-pass kernel: a 128-thread workgroup per walk, wave 0
-// solves the x axis and wave 1 the y axis (half the registers and twice the waves of the
-// one-wave kernel, for latency hiding); they share the staged z_ref, gain row and history
-// staging buffer, so loads and stores stay whole-walk coalesced.
+// Split-axis single-pass kernels: a 128-thread workgroup per walk, wave 0 solves the x axis
+// and wave 1 the y axis (half the registers and twice the waves of the one-wave kernel, for
+// latency hiding); they share the staged z_ref and the history staging rows, so loads and
+// stores stay whole-walk coalesced.
 template <int CW>
-__global__ void __launch_bounds__(128, 8) zmpc_rollout_unc_axis_kernel(RolloutArgs a) {
-  using ZL = ZrLayout<CW>;
-  constexpr int PF2 = (CW + 2) / 2;  // 128·PF2 >= 64·(CW+1) >= n
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  __shared__ int flag[2];
-  const int tid = threadIdx.x, axis = tid >> 6, lane = tid & 63;
-  const int64_t b = blockIdx.x;
-  const int n = a.n, nsteps = n - 1;
-  // k stays in global memory (wave-uniform scalar loads): at 8 waves per SIMD the scalar
-  // waits hide, and the LDS it would take keeps 16 walks per CU resident
-  const double* __restrict__ ks = a.k;
-  double* zr0 = smem;
-  double* zr1 = zr0 + a.lzp;
-  // ---- 1. bounds → z_ref (both waves, 128 samples per round) ---------------------------
-  {
-    const double2* zmx = reinterpret_cast<const double2*>(a.zmax + b * a.bstride);
-    const double2* zmn = reinterpret_cast<const double2*>(a.zmin + b * a.bstride);
-    double2 hi[PF2], lo[PF2];
-#pragma unroll
-    for (int u = 0; u < PF2; ++u) {
-      const int t = u * 128 + tid;
-      if (t < n && !(a.dbg & 8)) {
-        hi[u] = zmx[t];
-        lo[u] = zmn[t];
-      } else {
-        hi[u] = lo[u] = make_double2(0.0, 0.0);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < PF2; ++u) {
-      const int t = u * 128 + tid;
-      if (t < n) {
-        zr0[ZL::idx(t)] = (hi[u].x + lo[u].x) / 2;
-        zr1[ZL::idx(t)] = (hi[u].y + lo[u].y) / 2;
-      }
-    }
-    const double2 h = zmx[n - 1], l = zmn[n - 1];
-    const double last0 = (h.x + l.x) / 2, last1 = (h.y + l.y) / 2;
-    for (int t = n + tid; t < a.lz; t += 128) {
-      zr0[ZL::idx(t)] = last0;
-      zr1[ZL::idx(t)] = last1;
-    }
-  }
-  __syncthreads();
+struct AxisBounds {
+  static constexpr int PF2 = (CW + 2) / 2;  // 128·PF2 >= 64·(CW+1) >= n
+  double2 hi[PF2], lo[PF2];
+};
 
-  // ---- 2. correlation for this wave's axis --------------------------------------------
-  double f[CW];
-  {
-    const double* z = (axis ? zr1 : zr0) + ZL::idx(lane * CW);
-    double w[CW];
+template <int CW>
+__device__ __forceinline__ void axis_load(const RolloutArgs& a, int64_t b, int tid,
+                                          AxisBounds<CW>& r) {
+  const double2* zmx = reinterpret_cast<const double2*>(a.zmax + b * a.bstride);
+  const double2* zmn = reinterpret_cast<const double2*>(a.zmin + b * a.bstride);
 #pragma unroll
-    for (int m = 0; m < CW; ++m) {
-      f[m] = 0.0;
-      w[m] = z[ZL::idx(1 + m)];
-    }
-    for (int j = 0; j < ((a.dbg & 1) ? 0 : a.kc); j += CW) {
+  for (int u = 0; u < AxisBounds<CW>::PF2; ++u) {
+    const int t = u * 128 + tid;
+    // clamped rather than predicated (predicated double2 loads here crash the gfx950 backend
+    // of ROCm 7.2 in machine copy propagation); dbg bit 8 turns every load into row 0
+    const int tc = (a.dbg & 8) ? 0 : min(t, a.n - 1);
+    r.hi[u] = zmx[tc];
+    r.lo[u] = zmn[tc];
+  }
+}
+
+// z_ref rows of the walk into zr0/zr1; the last row also to last[2] (for the padding).
+template <int CW>
+__device__ __forceinline__ void axis_stage(const RolloutArgs& a, const AxisBounds<CW>& r,
+                                           double* zr0, double* zr1, double* last, int tid) {
+  using ZL = ZrLayout<CW>;
 #pragma unroll
-      for (int jj = 0; jj < CW; ++jj) {
-        const double kj = ks[j + jj];
-#pragma unroll
-        for (int m = 0; m < CW; ++m) f[m] = fma(kj, w[(jj + m) % CW], f[m]);
-        w[jj] = z[ZL::idx(1 + jj + CW)];
+  for (int u = 0; u < AxisBounds<CW>::PF2; ++u) {
+    const int t = u * 128 + tid;
+    if (t < a.n) {
+      const double v0 = (r.hi[u].x + r.lo[u].x) / 2, v1 = (r.hi[u].y + r.lo[u].y) / 2;
+      zr0[ZL::idx(t)] = v0;
+      zr1[ZL::idx(t)] = v1;
+      if (t == a.n - 1) {
+        last[0] = v0;
+        last[1] = v1;
       }
-      z += CW + ZL::kPad;
     }
   }
-  __syncthreads();  // z_ref is dead from here on: the area becomes the history staging
+}
+
+// The window padding (zmp_controller.py:81-88): rows n..lz-1 repeat the last row.
+template <int CW>
+__device__ __forceinline__ void axis_pad(const RolloutArgs& a, double* zr0, double* zr1,
+                                         const double* last, int tid) {
+  using ZL = ZrLayout<CW>;
+  const double l0 = last[0], l1 = last[1];
+  for (int t = a.n + tid; t < a.lz; t += 128) {
+    zr0[ZL::idx(t)] = l0;
+    zr1[ZL::idx(t)] = l1;
+  }
+}
+
+template <int CW>
+__device__ __forceinline__ void axis_correlate(const RolloutArgs& a, const double* __restrict__ ks,
+                                               const double* zr, int lane, double* f) {
+  using ZL = ZrLayout<CW>;
+  const double* z = zr + ZL::idx(lane * CW);
+  double w[CW];
+#pragma unroll
+  for (int m = 0; m < CW; ++m) {
+    f[m] = 0.0;
+    w[m] = z[ZL::idx(1 + m)];
+  }
+  for (int j = 0; j < ((a.dbg & 1) ? 0 : a.kc); j += CW) {
+#pragma unroll
+    for (int jj = 0; jj < CW; ++jj) {
+      const double kj = ks[j + jj];
+#pragma unroll
+      for (int m = 0; m < CW; ++m) f[m] = fma(kj, w[(jj + m) % CW], f[m]);
+      w[jj] = z[ZL::idx(1 + jj + CW)];
+    }
+    z += CW + ZL::kPad;
+  }
+}
+
+// Scan + replay + coalesced store of walk b's axis `axis` (f in registers); `stage` is the
+// walk's (dead) z_ref area, 2·lzp doubles, shared by both waves.
+template <int CW>
+__device__ __forceinline__ void axis_finish(const RolloutArgs& a, int64_t b, int tid,
+                                            const double* f, double* stage, int stage_rows,
+                                            int* flag) {
+  const int axis = tid >> 6, lane = tid & 63;
+  const int n = a.n, nsteps = n - 1;
   const double* xb = a.x0 + b * 6 + 3 * axis;
   const double xi[3] = {xb[0], xb[1], xb[2]};
   const double kk = (axis == 1 && a.kick != nullptr) ? a.kick[b] : 0.0;
   const int64_t kick_step = (axis == 1) ? a.kick_step : -1;
-
-  // ---- 3. lane-chunk affine scan (this axis) -----------------------------------------
   const LipmConsts lc = a.lc;
   const double kx0 = a.kx[0], kx1 = a.kx[1], kx2 = a.kx[2];
   const double Bv[3] = {lc.T3_6, lc.T2_2, lc.T};
@@ -511,6 +528,7 @@ __global__ void __launch_bounds__(128, 8) zmpc_rollout_unc_axis_kernel(RolloutAr
 #pragma unroll
       for (int j = 0; j < 3; ++j) Ab.m[3 * i + j] = A[3 * i + j] - Bv[i] * kx[j];
   }
+  // ---- lane-chunk affine scan ----------------------------------------------------------
   const int mbeg = lane * CW;
   double sv[3] = {0.0, 0.0, 0.0};
 #pragma unroll
@@ -524,7 +542,7 @@ __global__ void __launch_bounds__(128, 8) zmpc_rollout_unc_axis_kernel(RolloutAr
       if (mbeg + q == kick_step) sv[1] -= kk;
     }
   }
-  const double* Pp = a.scanP + (CW - 1) * 54;  // (Ā^CW)^(2^r), r = 0..5, from the plan
+  const double* Pp = a.scanP + (CW - 1) * kScanStride;  // (Ā^CW)^(2^r), r = 0..5, from the plan
   if (lane == 0) {
     double t[3];
     Mat3 P;
@@ -555,10 +573,8 @@ __global__ void __launch_bounds__(128, 8) zmpc_rollout_unc_axis_kernel(RolloutAr
     const double p = __shfl_up(sv[i], 1, 64);
     xs0[i] = (lane == 0) ? xi[i] : p;
   }
-
-  // ---- 4. replay (reference form) into the shared staging rows, coalesced copy-out ----
-  double* stage = zr0;
-  const int rows_per_round = (2 * a.lzp) / 6;
+  // ---- replay (reference form) into the shared staging rows, coalesced copy-out ------
+  const int rows_per_round = stage_rows;
   double* hb = a.hist + b * (int64_t)n * 6;
   double x[3];
   for (int r0 = 0; r0 < n; r0 += rows_per_round) {
@@ -604,6 +620,198 @@ __global__ void __launch_bounds__(128, 8) zmpc_rollout_unc_axis_kernel(RolloutAr
     if (lane == 0) flag[axis] = bad ? ZMPC_ST_NONFINITE : 0;
     __syncthreads();
     if (tid == 0) a.status[b] = flag[0] | flag[1];
+  }
+}
+
+// One walk per workgroup at 16 walks per CU (64 VGPRs): the history is staged through the
+// z_ref area, a.srows rows per round, the replay recomputed per round.
+template <int CW>
+__global__ void __launch_bounds__(128, 8) zmpc_rollout_unc_axis_kernel(RolloutArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  __shared__ int flag[2];
+  __shared__ double last[2];
+  const int tid = threadIdx.x, lane = tid & 63, axis = tid >> 6;
+  const int64_t b = blockIdx.x;
+  double* zr0 = smem;
+  double* zr1 = zr0 + a.lzp;
+  {
+    AxisBounds<CW> r;
+    axis_load<CW>(a, b, tid, r);
+    axis_stage<CW>(a, r, zr0, zr1, last, tid);
+  }
+  __syncthreads();
+  axis_pad<CW>(a, zr0, zr1, last, tid);
+  __syncthreads();
+  double f[CW];
+  axis_correlate<CW>(a, a.k, axis ? zr1 : zr0, lane, f);  // k: wave-uniform scalar loads
+  __syncthreads();  // z_ref is dead from here on: the area becomes the history staging
+  axis_finish<CW>(a, b, tid, f, zr0, a.srows, flag);
+}
+
+// Split-axis kernel, one walk per 128-thread workgroup with the fewest serial steps: every
+// global load (bounds, the last sample for the window padding, x0, kick) issued up front,
+// z_ref + padding in one pass, one replay writing the whole walk's history rows into the
+// dead z_ref area (LDS sized for it), and one coalesced copy-out — three barriers per walk.
+// One walk of the split kernel (shared by the one-walk-per-workgroup and the persistent
+// launch).  The tables read on wave-uniform addresses come in as __restrict__ pointers so the
+// compiler keeps them on scalar loads even inside a loop that stores the history.
+template <int CW>
+__device__ __forceinline__ void split_walk(const RolloutArgs& a, int64_t b, double* smem,
+                                           int* flag, const double* __restrict__ kg,
+                                           const double* __restrict__ scanP,
+                                           const double* __restrict__ kxp,
+                                           double* __restrict__ hist) {
+  using ZL = ZrLayout<CW>;
+  const int tid = threadIdx.x, lane = tid & 63, axis = tid >> 6;
+  const int n = a.n, nsteps = n - 1;
+  double* zr0 = smem;
+  double* zr1 = zr0 + a.lzp;
+  // ---- 1. loads ----------------------------------------------------------------------------
+  AxisBounds<CW> r;
+  axis_load<CW>(a, b, tid, r);
+  const double2 hl = reinterpret_cast<const double2*>(a.zmax + b * a.bstride)[n - 1];
+  const double2 ll = reinterpret_cast<const double2*>(a.zmin + b * a.bstride)[n - 1];
+  const double* xb = a.x0 + b * 6 + 3 * axis;
+  const double xi[3] = {xb[0], xb[1], xb[2]};
+  const double kk = (axis == 1 && a.kick != nullptr) ? a.kick[b] : 0.0;
+  // ---- 2. z_ref rows + window padding (zmp_controller.py:81-88) ----------------------------
+#pragma unroll
+  for (int u = 0; u < AxisBounds<CW>::PF2; ++u) {
+    const int t = u * 128 + tid;
+    if (t < n) {
+      zr0[ZL::idx(t)] = (r.hi[u].x + r.lo[u].x) / 2;
+      zr1[ZL::idx(t)] = (r.hi[u].y + r.lo[u].y) / 2;
+    }
+  }
+  {
+    const double l0 = (hl.x + ll.x) / 2, l1 = (hl.y + ll.y) / 2;
+    for (int t = n + tid; t < a.lz; t += 128) {
+      zr0[ZL::idx(t)] = l0;
+      zr1[ZL::idx(t)] = l1;
+    }
+  }
+  __syncthreads();
+  // ---- 3. correlation (this wave's axis) ---------------------------------------------------
+  double f[CW];
+  axis_correlate<CW>(a, kg, axis ? zr1 : zr0, lane, f);  // k: wave-uniform scalar loads
+  __syncthreads();  // z_ref dead: the area becomes the history staging (n rows of 6)
+  // ---- 4. lane-chunk affine scan -----------------------------------------------------------
+  const int64_t kick_step = (axis == 1) ? a.kick_step : -1;
+  const LipmConsts lc = a.lc;
+  const double kx0 = kxp[0], kx1 = kxp[1], kx2 = kxp[2];
+  const double Bv[3] = {lc.T3_6, lc.T2_2, lc.T};
+  Mat3 Ab;
+  {
+    const double A[9] = {1.0, lc.T, lc.T2_2, 0.0, 1.0, lc.T, 0.0, 0.0, 1.0};
+    const double kx[3] = {kx0, kx1, kx2};
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) Ab.m[3 * i + j] = A[3 * i + j] - Bv[i] * kx[j];
+  }
+  const int mbeg = lane * CW;
+  double sv[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+  for (int q = 0; q < CW; ++q) {
+    if (mbeg + q < nsteps) {
+      double t[3];
+      matvec3(Ab, sv, t);
+      sv[0] = fma(Bv[0], f[q], t[0]);
+      sv[1] = fma(Bv[1], f[q], t[1]);
+      sv[2] = fma(Bv[2], f[q], t[2]);
+      if (mbeg + q == kick_step) sv[1] -= kk;
+    }
+  }
+  const double* Pp = scanP + (CW - 1) * kScanStride;  // (Ā^CW)^(2^r), r = 0..5, from the plan
+  if (lane == 0) {
+    double t[3];
+    Mat3 P;
+#pragma unroll
+    for (int q = 0; q < 9; ++q) P.m[q] = Pp[q];
+    matvec3(P, xi, t);
+    for (int i = 0; i < 3; ++i) sv[i] += t[i];
+  }
+#pragma unroll
+  for (int r2 = 0; r2 < 6; ++r2) {
+    const int d = 1 << r2;
+    if (a.dbg & 2) break;
+    double u[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) u[i] = __shfl_up(sv[i], d, 64);
+    if (lane >= d) {
+      Mat3 Pd;
+#pragma unroll
+      for (int q = 0; q < 9; ++q) Pd.m[q] = Pp[r2 * 9 + q];
+      double t[3];
+      matvec3(Pd, u, t);
+      for (int i = 0; i < 3; ++i) sv[i] += t[i];
+    }
+  }
+  double x[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const double p = __shfl_up(sv[i], 1, 64);
+    x[i] = (lane == 0) ? xi[i] : p;
+  }
+  // ---- 5. replay (reference form) straight into the staged history ------------------------
+  double* stage = smem;
+  if (lane == 0) {
+    stage[3 * axis + 0] = xi[0];
+    stage[3 * axis + 1] = xi[1];
+    stage[3 * axis + 2] = xi[2];
+  }
+#pragma unroll
+  for (int q = 0; q < CW; ++q) {
+    const int m = mbeg + q;
+    if (m < nsteps) {
+      const double u = f[q] - (kx0 * x[0] + kx1 * x[1] + kx2 * x[2]);
+      double xn[3];
+      lipm_step(lc, x, u, xn);
+      if (m == kick_step) xn[1] -= kk;
+      double* o = stage + (m + 1) * 6 + 3 * axis;
+      o[0] = xn[0];
+      o[1] = xn[1];
+      o[2] = xn[2];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) x[i] = xn[i];
+    }
+  }
+  if (a.status != nullptr) {
+    const bool finite = isfinite(x[0]) && isfinite(x[1]) && isfinite(x[2]);
+    const unsigned long long bad = __ballot(!finite);
+    if (lane == 0) flag[axis] = bad ? ZMPC_ST_NONFINITE : 0;
+  }
+  __syncthreads();
+  // ---- 6. coalesced copy-out ---------------------------------------------------------------
+  if (!(a.dbg & 4)) {
+    const double2* src = reinterpret_cast<const double2*>(stage);
+    double2* dst = reinterpret_cast<double2*>(hist + b * (int64_t)n * 6);
+    for (int e = tid; e < n * 3; e += 128) dst[e] = src[e];
+  }
+  if (a.status != nullptr && tid == 0) a.status[b] = flag[0] | flag[1];
+}
+
+
+template <int CW>
+__global__ void __launch_bounds__(128, 4) zmpc_rollout_unc_split_kernel(RolloutArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  __shared__ int flag[2];
+  split_walk<CW>(a, blockIdx.x, smem, flag, a.k, a.scanP, a.kx, a.hist);
+}
+
+// Persistent form: grid = resident workgroups (occupancy × CUs), walks strided over it — the
+// workgroups drift out of phase after the first walk, so one's history stores overlap
+// another's correlation (config 2: 45 µs vs 50 µs one walk per workgroup).
+template <int CW>
+__global__ void __launch_bounds__(128, 4)
+    zmpc_rollout_unc_pers_kernel(RolloutArgs a, const double* __restrict__ kg,
+                                 const double* __restrict__ scanP,
+                                 const double* __restrict__ kxp, double* __restrict__ hist) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  __shared__ int flag[2];
+  for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x) {
+    split_walk<CW>(a, b, smem, flag, kg, scanP, kxp, hist);
+    __syncthreads();  // staging read out before the next walk's z_ref overwrites it
   }
 }
 
@@ -705,15 +913,38 @@ int g_cus = 0;  // CUs of the device the attributes were set on (grid sizing)
 
 template <int CW>
 void launch_unc(const RolloutGeom& g, size_t lds, hipStream_t s, const RolloutArgs& a) {
-  static const bool one_wave = [] {
-    const char* e = getenv("ZMPC_ROLLOUT_ONEWAVE");  // diagnostic A/B: one wave per walk
-    return e != nullptr && atoi(e) != 0;
+  // Kernel choice; ZMPC_ROLLOUT_VARIANT overrides it for A/B runs (DESIGN.md §4 has the
+  // config-2 measurements): 8 = split, persistent grid (default); 6 = split, one walk per
+  // workgroup; 1 = split-axis at 16 walks per CU staging through the z_ref area; 2 = one wave
+  // per walk.  All single-pass kernels produce identical histories (tests/test_gpu_parity.py).
+  static const int variant = [] {
+    const char* e = getenv("ZMPC_ROLLOUT_VARIANT");
+    return e ? atoi(e) : 8;
   }();
-  // the split-axis kernel is built for 8 waves/SIMD: it keeps the default 64 KiB LDS cap
   const size_t lds_axis = lds - (size_t)a.kcp * sizeof(double);  // no staged gain row
-  if (g.passes == 1 && !one_wave && lds_axis <= 64 * 1024) {
+  const size_t lds_split = std::max<size_t>(lds_axis, 6 * (size_t)a.n * sizeof(double));
+  RolloutArgs b = a;
+  if (g.passes == 1 && (variant == 8 || variant == 6) && lds_split <= 64 * 1024) {
+    int per_cu = 0;
+    if (variant == 8 &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per_cu, reinterpret_cast<const void*>(zmpc_rollout_unc_pers_kernel<CW>), 128,
+            lds_split) != hipSuccess)
+      per_cu = 0;
+    const int64_t grid = (int64_t)std::max(g_cus, 1) * per_cu;
+    // persistent only for a few walks per workgroup: config 2 (2 per workgroup) 45 µs vs
+    // 49 µs; at 8 per workgroup (B = 16384) the one-walk grid is faster (156 vs 177 µs)
+    if (per_cu > 0 && grid < a.B && a.B <= 3 * grid) {
+      hipLaunchKernelGGL(zmpc_rollout_unc_pers_kernel<CW>, dim3((unsigned)grid), dim3(128),
+                         lds_split, s, a, a.k, a.scanP, a.kx, a.hist);
+    } else {
+      hipLaunchKernelGGL(zmpc_rollout_unc_split_kernel<CW>, dim3((unsigned)a.B), dim3(128),
+                         lds_split, s, a);
+    }
+  } else if (g.passes == 1 && variant != 2 && lds_axis <= 64 * 1024) {
+    b.srows = (int)(lds_axis / (6 * sizeof(double)));
     hipLaunchKernelGGL(zmpc_rollout_unc_axis_kernel<CW>, dim3((unsigned)a.B), dim3(128), lds_axis,
-                       s, a);
+                       s, b);
   } else if (g.passes == 1) {
     hipLaunchKernelGGL(zmpc_rollout_unc_kernel<CW>, dim3((unsigned)a.B), dim3(64), lds, s, a);
   } else {
@@ -750,7 +981,7 @@ hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, con
   }();
   RolloutArgs a{g.kc, g.kcp, g.lz,      g.lzp, (int)n,     B,   p->lc,
                 p->k, p->kx,  zmax,      zmin,  bstride,    x0,  kick,
-                kick_step,    hist, status, p->scanP, dbg};
+                kick_step,    hist, status, p->scanP, dbg, 0};
   switch (g.cw) {
 #define ZMPC_CW(C)               \
   case C:                        \

@@ -10,6 +10,11 @@
 
 // Scalar LIPM constants of zmp_controller.py:18-20 (A = [[1,T,T²/2],[0,1,T],[0,0,1]],
 // B = [T³/6, T²/2, T]ᵀ), evaluated on the host as Python evaluates them.
+// Rollout scan propagators per chunk width C = 1..8: (Ā^C)^(2^r), r = 0..kScanLevels-1
+// (64-lane Kogge-Stone rounds use r <= 5; the 128-lane kernels' cross-wave offset uses r = 6).
+constexpr int kScanLevels = 7;
+constexpr int kScanStride = kScanLevels * 9;
+
 struct LipmConsts {
   double T;     // A[0,1] = A[1,2] = B[2]
   double T2_2;  // A[0,2] = B[1]
@@ -30,7 +35,7 @@ struct zmpc_plan {
   double* L = nullptr;   // [N,N] lower Cholesky factor of M
   double* k = nullptr;   // [Kpad] gain row e0ᵀ M⁻¹ Puᵀ (zero-padded)
   double* kx = nullptr;  // [3]  k·Px
-  double* scanP = nullptr;  // [8][6][9] (Ā^C)^(2^r) rollout scan propagators
+  double* scanP = nullptr;  // [8][kScanLevels][9] (Ā^C)^(2^r) rollout scan propagators
   double* X = nullptr;   // [N,N] L⁻¹ Puᵀ (strict plans)
   double* G = nullptr;   // [N,N] Pu (R I + Q PuᵀPu)⁻¹ Puᵀ (strict plans)
   double* v = nullptr;   // [N]   first column of Pu⁻¹ (strict plans)

@@ -24,16 +24,16 @@ for a, b in ev:
     a.record(); L(); b.record()
 torch.cuda.synchronize()
 print(json.dumps(dict(B=B, N=N, n=n, dbg=os.environ.get("ZMPC_DEBUG_ROLLOUT", "0"),
-                      onewave=os.environ.get("ZMPC_ROLLOUT_ONEWAVE", "0"),
+                      variant=os.environ.get("ZMPC_ROLLOUT_VARIANT", "8"),
                       us=float(np.median([a.elapsed_time(b) for a, b in ev])) * 1e3)))
 '''
 
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 env0 = dict(os.environ, PKG=os.path.join(root, "model-predictive-control-for-bipedal-locomotion_amd"))
-VARIANTS = [dict(), dict(ZMPC_ROLLOUT_ONEWAVE="1")]
+VARIANTS = [dict(ZMPC_ROLLOUT_VARIANT=v) for v in ("8", "6", "1", "2")]
 for B, N, n in [(1024, 150, 420), (4096, 150, 420), (16384, 150, 420)]:
   for var in VARIANTS:
-    for dbg in (0, 1, 15):
+    for dbg in ((0, 1, 15) if B == 4096 else (0,)):
         env = dict(env0, ZMPC_DEBUG_ROLLOUT=str(dbg), **var)
         r = subprocess.run([sys.executable, "-c", CHILD, str(B), str(N), str(n)], env=env,
                            capture_output=True, text=True, timeout=120)

@@ -4,11 +4,13 @@ Tolerances: north_star's bar is CoM/ZMP RMSE <= 1e-6 against the reference NumPy
 unconstrained path is held to 1e-9 here (the reference's own BLAS noise floor is ~7e-13), the
 strict path to 1e-6 against the exact KKT-certified oracle (parity with OSQP unpinned).
 """
+import os
+
 import numpy as np
 import pytest
 import torch
 
-from conftest import golden, rmse
+from conftest import PKG, golden, rmse
 from oracle import zmp_oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -188,6 +190,57 @@ def test_empty_batch():
     p = plan(64)
     hist, st = p.rollout(np.zeros((0, 10, 2)), np.zeros((0, 10, 2)), np.zeros((0, 2, 3)))
     assert hist.shape == (0, 10, 2, 3)
+
+
+@pytest.mark.parametrize("n", (65, 420))
+def test_multi_walk_workgroups_vs_oracle(n):
+    """More walks than resident workgroups (B > 16 per CU x CUs, several dispatch rounds),
+    every walk distinct, all checked."""
+    B = 2 * 16 * torch.cuda.get_device_properties(0).multi_processor_count + 37
+    rng = np.random.default_rng(n + 7)
+    N = 150
+    dt = 1.5 / N
+    ctr = np.cumsum(rng.normal(0, 0.01, (B, n, 2)), 1)
+    zmax, zmin = ctr + rng.uniform(0.02, 0.08, (B, 1, 2)), ctr - 0.05
+    x0 = rng.normal(0, 0.01, (B, 2, 3))
+    kick = rng.uniform(-0.2, 0.2, B)
+    p = plan(N, dt=dt)
+    hist, st = p.rollout(zmax, zmin, x0, kick=kick, kick_step=n // 3)
+    ref = O.rollout_gain(zmax, zmin, x0, N, dt, H, G, Q, R, kick, n // 3)
+    assert np.abs(hist.cpu().numpy() - ref).max() <= 1e-8
+    assert int(st.abs().max()) == 0
+
+
+_VARIANT_CHILD = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, sys.argv[1])
+from mpc_bipedal.solver import Plan
+d = np.load(sys.argv[2])
+p = Plan(0, 150, float(d["dt"]), 0.75, 9.81, 1.0, 1e-6, False)
+h, _ = p.rollout(d["zmax"], d["zmin"], d["x0"], kick=d["kick"], kick_step=int(d["ks"]))
+np.save(sys.argv[3], h.cpu().numpy())
+"""
+
+
+def test_rollout_kernel_variants_agree(tmp_path):
+    """The single-pass kernels (ZMPC_ROLLOUT_VARIANT 8 split persistent — the default, 6 split
+    one walk per workgroup, 1 split-axis with z_ref-area staging, 2 one wave per walk) agree."""
+    import subprocess
+    import sys
+    zmax, zmin, x0, F, dt = synthetic_batch(4133, 150)
+    n = zmax.shape[1]
+    kick = dt * F / M
+    inp = tmp_path / "in.npz"
+    np.savez(inp, zmax=zmax, zmin=zmin, x0=x0, kick=kick, ks=n // 2, dt=dt)
+    outs = []
+    for v in (8, 6, 1, 2):
+        out = tmp_path / f"h{v}.npy"
+        env = dict(os.environ, ZMPC_ROLLOUT_VARIANT=str(v))
+        subprocess.run([sys.executable, "-c", _VARIANT_CHILD, PKG, str(inp), str(out)],
+                       env=env, check=True, timeout=300)
+        outs.append(np.load(out))
+    for o in outs[1:]:
+        assert np.abs(outs[0] - o).max() <= 1e-12
 
 
 def test_full_size_config2_properties():
