@@ -1,15 +1,21 @@
 #!/usr/bin/env python3
 """Benchmark: QP solves/s of the batched Wieber LIPM-ZMP MPC on MI355X.
 
-Workload (BASELINE.json configs[1]): per GPU, a batch of B = 4096
-default.json walks (n = 420 CoP samples, horizon N = 150, dt = 0.01, unconstrained solve),
-each with a rigid CoP offset δ_b ~ U(−0.02, 0.02)² m, x0 position ~ U(−0.01, 0.01) and an
-F_ext_b ~ U(0, 800) N kick at step n//2; walk 0 is the reference walk (δ = 0, x0 = 0,
-F = 400 N).  One "step" of this bench = one batched rollout of every walk over all n−1
-timesteps and both axes = B·(n−1)·2 QP solves, inputs already resident in HBM.
+Workloads (`--config`, default 2 = BASELINE.json's metric configuration):
+  2  per GPU B = 4096 default.json walks (n = 420 CoP samples, horizon N = 150, dt = 0.01),
+     unconstrained; each walk a rigid CoP offset δ_b ~ U(−0.02, 0.02)² m, x0 position
+     ~ U(−0.01, 0.01), an F_ext_b ~ U(0, 800) N kick at step n//2; walk 0 is the reference
+     walk (δ = 0, x0 = 0, F = 400 N).
+  3  as 2 with strict = True (box-constrained QP), per GPU B = 65536.
+  4  Monte-Carlo F_ext: one shared default.json CoP broadcast to every scenario
+     (bounds_stride 0), x0 = 0, F ~ U(0, 800) N, strict; per GPU 125 000 scenarios
+     (`--unconstrained` for the unconstrained variant).
+  5  horizon N = 512 (dt = 1.5/512, n = 1431), offsets as 2, unconstrained, per GPU 2048.
+One "step" = one batched rollout of every walk over all n−1 timesteps and both axes
+= B·(n−1)·2 QP solves, inputs already resident in HBM.
 
 Multi-GPU (torchrun, one process per GPU, RCCL): weak scaling, each rank rolls out its own
-4096-walk block with no data-path collective; the CoM all-gather that reassembles the full
+block of walks with no data-path collective; the CoM all-gather that reassembles the full
 trajectories is timed separately (allgather_ms), outside `value`.
 
 Prints ONE JSON line (rank 0).
@@ -42,12 +48,27 @@ DEFAULT_JSON = dict(ssp_duration=0.24, dsp_duration=0.03, standing_duration=1.0,
                     g=9.81, m=40.0, F_ext=400.0, strict=True, add_force=True)
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 FP64_PEAK_TFS = 78.6    # FP64 vector = matrix peak (spec)
+FP64_SUSTAINED_TFS = 56.6  # profiles/r1_fp64_peak.log: register-only FMA chains, 8 waves/SIMD
 SEED = 20251226
 
 
-def make_batch(B, rank, cfg, strict):
+CONFIGS = {
+    2: dict(batch=4096, horizon=150, strict=False, shared=False),
+    3: dict(batch=65536, horizon=150, strict=True, shared=False),
+    4: dict(batch=125000, horizon=150, strict=True, shared=True),
+    5: dict(batch=2048, horizon=512, strict=False, shared=False),
+}
+
+
+def make_batch(B, rank, cfg, shared):
+    """Bounds ([B,n,2] per walk, or the shared [n,2] CoP), x0 [B,2,3], F [B]."""
     zmax, zmin, _ = CoPGenerator(cfg).generate_cop_trajectory()
     rng = np.random.default_rng(SEED + 7919 * rank)
+    if shared:  # config 4: x0 = 0, one CoP for every scenario
+        F = rng.uniform(0.0, 800.0, B)
+        if rank == 0:
+            F[0] = 400.0
+        return zmax, zmin, zmax, zmin, np.zeros((B, 2, 3)), F
     off = rng.uniform(-0.02, 0.02, (B, 1, 2))
     x0 = np.zeros((B, 2, 3))
     x0[:, :, 0] = rng.uniform(-0.01, 0.01, (B, 2))
@@ -57,45 +78,91 @@ def make_batch(B, rank, cfg, strict):
     return zmax, zmin, zmax[None] + off, zmin[None] + off, x0, F
 
 
+def walk_bounds(zmax_b, zmin_b, b):
+    """Walk b's [n,2] bounds from a per-walk [B,n,2] or a shared [n,2] array."""
+    if zmax_b.ndim == 2:
+        return zmax_b, zmin_b
+    return zmax_b[b], zmin_b[b]
+
+
 def cpu_baseline(zmax_b, zmin_b, x0_b, kick_b, hist_gpu, cfg, budget_s):
-    """Reference-faithful NumPy port (oracle/zmp_oracle.py:predict_wieber_axis_ref: the
-    interpreted Px/Pu build + np.linalg.inv of zmp_controller.py:162-199, per solve), one
-    BLAS thread, on whole walks of the same batch until `budget_s` of CPU work is spent."""
+    """CPU path beside the GPU run (rank 0, N=1).  This leg is the only place bench.py touches
+    oracle/ — as the checker and the timed CPU baseline, never as the measured product.
+      * value: the reference-faithful NumPy port (oracle predict_wieber_axis_ref: interpreted
+        Px/Pu build + np.linalg.inv per solve, zmp_controller.py:162-199; strict: the exact
+        active-set box-QP restatement — the reference's cvxpy/OSQP is not installed), one BLAS
+        thread, whole walks of this batch until `budget_s` of CPU work is spent;
+      * optimized: the batched gain-form port (oracle rollout_gain, all BLAS threads) on the
+        first walks (unconstrained configs);
+      * parity: GPU vs port on those walks (CoM RMSE, max |Δstate|)."""
     from oracle import zmp_oracle as O
     from threadpoolctl import threadpool_limits
     with threadpool_limits(1):
-        return _cpu_baseline(O, zmax_b, zmin_b, x0_b, kick_b, hist_gpu, cfg, budget_s)
+        out = _cpu_baseline(O, zmax_b, zmin_b, x0_b, kick_b, hist_gpu, cfg, budget_s)
+    if not cfg.strict:
+        nb = min(64, len(x0_b))
+        zx = zmax_b if zmax_b.ndim == 3 else np.broadcast_to(zmax_b, (nb,) + zmax_b.shape)
+        zn = zmin_b if zmin_b.ndim == 3 else np.broadcast_to(zmin_b, (nb,) + zmin_b.shape)
+        n = zx.shape[1]
+        t0 = time.perf_counter()
+        ref = O.rollout_gain(zx[:nb], zn[:nb], x0_b[:nb], cfg.horizon, cfg.dt, cfg.h, cfg.g,
+                             cfg.Q, cfg.R, kick_b[:nb], n // 2)
+        tg = time.perf_counter() - t0
+        out["optimized"] = {"value": nb * (n - 1) * 2 / tg, "unit": "QP solves/s",
+                            "cores": os.cpu_count(), "kind": "port",
+                            "sample": f"first {nb} walks, batched gain-form NumPy port "
+                                      "(oracle rollout_gain), default BLAS threads"}
+        out["parity_first_walks"] = {
+            "walks": nb,
+            "com_rmse": float(np.sqrt(np.mean((hist_gpu[:nb, :, :, 0] - ref[..., 0]) ** 2))),
+            "max_abs_state": float(np.abs(hist_gpu[:nb] - ref).max())}
+    return out
 
 
 def _cpu_baseline(O, zmax_b, zmin_b, x0_b, kick_b, hist_gpu, cfg, budget_s):
     N, dt = cfg.horizon, cfg.dt
     solves, elapsed, walks, rms = 0, 0.0, 0, []
-    b = 1
-    while elapsed < budget_s and b < len(zmax_b):
-        n = zmax_b.shape[1]
-        zx = np.vstack([zmax_b[b], np.tile(zmax_b[b, -1:], (N, 1))])
-        zn = np.vstack([zmin_b[b], np.tile(zmin_b[b, -1:], (N, 1))])
-        x = x0_b[b, 0].reshape(3, 1).copy()
-        y = x0_b[b, 1].reshape(3, 1).copy()
-        com = [[x[0, 0], y[0, 0]]]
+    b = 1 if len(x0_b) > 1 else 0
+    first = b
+    while elapsed < budget_s and b < len(x0_b):
+        zmx, zmn = walk_bounds(zmax_b, zmin_b, b)
+        n = zmx.shape[0]
         t0 = time.perf_counter()
-        for i in range(n - 1):
-            x = O.predict_wieber_axis_ref(x, N, zx[i + 1:i + 1 + N, 0:1], zn[i + 1:i + 1 + N, 0:1],
-                                          dt, cfg.h, cfg.g, cfg.Q, cfg.R)
-            y = O.predict_wieber_axis_ref(y, N, zx[i + 1:i + 1 + N, 1:2], zn[i + 1:i + 1 + N, 1:2],
-                                          dt, cfg.h, cfg.g, cfg.Q, cfg.R)
-            if i == n // 2:
-                y = y - np.array([[0.0, kick_b[b], 0.0]]).T
-            com.append([x[0, 0], y[0, 0]])
+        if cfg.strict:
+            h = O.rollout_strict(x0_b[b, 0], x0_b[b, 1], zmx, zmn, N, dt, cfg.h, cfg.g, cfg.Q,
+                                 cfg.R, kick=kick_b[b], kick_step=n // 2)
+            com = h[:, :, 0]
+        else:
+            zx = np.vstack([zmx, np.tile(zmx[-1:], (N, 1))])
+            zn = np.vstack([zmn, np.tile(zmn[-1:], (N, 1))])
+            x = x0_b[b, 0].reshape(3, 1).copy()
+            y = x0_b[b, 1].reshape(3, 1).copy()
+            com = [[x[0, 0], y[0, 0]]]
+            for i in range(n - 1):
+                if elapsed + time.perf_counter() - t0 > budget_s and i >= 16:
+                    break  # long walks (config 5): a timed prefix of the walk
+                x = O.predict_wieber_axis_ref(x, N, zx[i + 1:i + 1 + N, 0:1],
+                                              zn[i + 1:i + 1 + N, 0:1], dt, cfg.h, cfg.g,
+                                              cfg.Q, cfg.R)
+                y = O.predict_wieber_axis_ref(y, N, zx[i + 1:i + 1 + N, 1:2],
+                                              zn[i + 1:i + 1 + N, 1:2], dt, cfg.h, cfg.g,
+                                              cfg.Q, cfg.R)
+                if i == n // 2:
+                    y = y - np.array([[0.0, kick_b[b], 0.0]]).T
+                com.append([x[0, 0], y[0, 0]])
+            com = np.array(com)
         elapsed += time.perf_counter() - t0
-        solves += 2 * (n - 1)
-        rms.append(float(np.sqrt(np.mean((np.array(com) - hist_gpu[b, :, :, 0]) ** 2))))
+        solves += 2 * (len(com) - 1)
+        rms.append(float(np.sqrt(np.mean((com - hist_gpu[b, :len(com), :, 0]) ** 2))))
         walks += 1
         b += 1
+    what = ("exact active-set box-QP NumPy port (oracle rollout_strict; the reference's "
+            "cvxpy/OSQP is not installed)" if cfg.strict else
+            "reference-faithful NumPy port (interpreted Pu build + np.linalg.inv per solve, "
+            "zmp_controller.py:162-199)")
     return dict(value=solves / elapsed, unit="QP solves/s", cores=1, kind="port",
-                sample=f"{walks} full walk(s) = {solves} solves of this batch (walks 1..{walks}), "
-                       "reference-faithful NumPy port (interpreted Pu build + np.linalg.inv "
-                       "per solve, zmp_controller.py:162-199), 1 BLAS thread",
+                sample=f"{walks} walk(s) = {solves} solves of this batch (walks "
+                       f"{first}..{first + walks - 1}), {what}, 1 BLAS thread",
                 seconds=elapsed, com_rmse_gpu_vs_port=max(rms) if rms else None)
 
 
@@ -115,9 +182,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=4096, help="walks per GPU")
-    ap.add_argument("--horizon", type=int, default=150)
-    ap.add_argument("--strict", action="store_true", help="strict ZMP box constraints (config 3)")
+    ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS),
+                    help="SURVEY.md §8d workload (2 = BASELINE.json metric config)")
+    ap.add_argument("--batch", type=int, default=None, help="walks per GPU (config default)")
+    ap.add_argument("--horizon", type=int, default=None)
+    ap.add_argument("--strict", action="store_true", help="alias of --config 3")
+    ap.add_argument("--unconstrained", action="store_true", help="config 4 unconstrained variant")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
@@ -132,13 +202,17 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
 
+    conf = 3 if args.strict else args.config
+    wl = dict(CONFIGS[conf])
+    if args.unconstrained:
+        wl["strict"] = False
     d = dict(DEFAULT_JSON)
-    d["horizon"] = args.horizon
-    d["strict"] = bool(args.strict)
+    d["horizon"] = args.horizon or wl["horizon"]
+    d["strict"] = wl["strict"]
     cfg = MPCConfig(**d)  # dt = 1.5 / horizon
-    B = args.batch
-    cop_x, cop_n, zmax_h, zmin_h, x0_h, F_h = make_batch(B, rank, cfg, args.strict)
-    n = zmax_h.shape[1]
+    B = args.batch or wl["batch"]
+    cop_x, cop_n, zmax_h, zmin_h, x0_h, F_h = make_batch(B, rank, cfg, wl["shared"])
+    n = zmax_h.shape[-2]
     kick_h = cfg.dt * F_h / cfg.m
     plan = Plan(dev.index, cfg.horizon, cfg.dt, cfg.h, cfg.g, cfg.Q, cfg.R, cfg.strict)
     zmax = torch.as_tensor(zmax_h, device=dev)
@@ -179,12 +253,14 @@ def main():
 
     solves_per_step = B * (n - 1) * 2 * world
     value = solves_per_step * args.steps / elapsed
-    # algorithmic bytes of one launch: bounds in (2 × [B,n,2] f64) + history out ([B,n,2,3])
-    alg_bytes = 2 * B * n * 2 * 8 + B * n * 6 * 8
+    # algorithmic bytes of one launch: bounds in (2 × [B,n,2] f64, or one shared [n,2] pair)
+    # + history out ([B,n,2,3])
+    alg_bytes = 2 * (1 if wl["shared"] else B) * n * 2 * 8 + B * n * 6 * 8
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     flops = B * (n - 1) * 2 * (2 * cfg.horizon + 20)
     gemm_tf = B * (n - 1) * 2 * 2 * cfg.horizon ** 2 / (kern_ms * 1e-3) / 1e12
-    workload = ("config3_strict" if args.strict else "config2") + f"_n{cfg.horizon}_b{B}"
+    workload = (f"config{conf}" + ("_unc" if conf == 4 and not cfg.strict else "") +
+                f"_n{cfg.horizon}_b{B}")
 
     # parity in the same run: the reference walk (walk 0 of rank 0) vs the committed
     # reference fixture (tests/golden: produced by the reference itself)
@@ -192,7 +268,7 @@ def main():
     if rank == 0 and cfg.horizon == 150:
         fx = np.load(os.path.join(ROOT, "tests", "golden", "walk_n150.npz"))
         ref_com = fx["com_force"]
-        if not args.strict and ref_com.shape[0] == n:
+        if not cfg.strict and ref_com.shape[0] == n:
             com_rmse_ref = float(np.sqrt(np.mean(
                 (hist[0, :, :, 0].cpu().numpy() - ref_com) ** 2)))
 
@@ -207,14 +283,29 @@ def main():
         gather_ms = (time.perf_counter() - tg) * 1e3
         assert full.shape[0] == B * world
 
+    # the drop-in batch API hands host arrays over: PCIe-inclusive rate (never `value`)
+    pcie = None
+    if rank == 0 and world == 1:
+        reps = 1 if cfg.strict else 3
+        torch.cuda.synchronize()
+        tp = time.perf_counter()
+        for _ in range(reps):
+            h, st = plan.rollout(zmax_h, zmin_h, x0_h, kick=kick_h, kick_step=kstep)
+            h.cpu()
+        torch.cuda.synchronize()
+        tp = (time.perf_counter() - tp) / reps
+        pcie = {"value": B * (n - 1) * 2 / tp, "unit": "QP solves/s", "ms_per_step": tp * 1e3,
+                "path": "Plan.rollout(numpy in) + hist.cpu(): pageable H2D of bounds/x0/kick, "
+                        "kernel, D2H of the history"}
+
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.strict:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(zmax_h, zmin_h, x0_h, kick_h, hist.cpu().numpy(), cfg,
                            args.cpu_seconds)
 
     if rank == 0:
         traffic = pmc_traffic(workload)
-        if not args.strict:
+        if not cfg.strict:
             roof = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": achieved / HBM_PEAK_GBS}
         else:
@@ -223,10 +314,11 @@ def main():
                     "unit": "TFLOP/s", "frac": gemm_tf / FP64_PEAK_TFS}
         roof.update({
             "traffic": traffic,
-            "kernel": "zmpc_strict_kernel" if args.strict else "zmpc_rollout_unc_kernel",
+            "kernel": "zmpc_strict_kernel" if cfg.strict else "zmpc_rollout_unc_kernel",
             "kernel_ms": kern_ms, "alg_bytes_per_launch": alg_bytes,
             "hbm_gbs": achieved, "alg_flops_per_launch": flops,
-            "fp64_frac_alg": flops / (kern_ms * 1e-3) / (FP64_PEAK_TFS * 1e12)})
+            "fp64_frac_alg": flops / (kern_ms * 1e-3) / (FP64_PEAK_TFS * 1e12),
+            "fp64_sustained_peak_tfs": FP64_SUSTAINED_TFS})
         line = {
             "metric": "QP solves/sec (horizon=150, batched) at 1/2/4/8 MI355X; CoM RMSE vs ref",
             "value": value,
@@ -241,17 +333,21 @@ def main():
             "dtype": "f64",
             "data": "synthetic (default.json CoP + seeded offsets/x0/F_ext, SURVEY.md §8d)",
             "config": {
-                "workload": ("config3: B strict walks" if args.strict else
-                             "config2: B default.json walks, unconstrained") +
-                            f", horizon={cfg.horizon}, n={n}",
+                "workload": f"config{conf}: " + (
+                    "shared default.json CoP, Monte-Carlo F_ext" if wl["shared"] else
+                    "default.json walks + rigid offsets") +
+                    (", strict" if cfg.strict else ", unconstrained") +
+                    f", horizon={cfg.horizon}, n={n}",
                 "walks_per_gpu": B, "global_batch": B * world, "horizon": cfg.horizon,
                 "samples_per_walk": n, "solves_per_step": solves_per_step,
-                "parallelism": f"dp{world}", "strict": bool(args.strict),
+                "parallelism": f"dp{world}", "strict": bool(cfg.strict),
+                "shared_cop": bool(wl["shared"]),
             },
             "roofline": roof,
             "cpu_baseline": cpu,
             "com_rmse_vs_ref": com_rmse_ref,
             "allgather_ms": gather_ms,
+            "pcie_inclusive": pcie,
         }
         print(json.dumps(line))
     if world > 1:

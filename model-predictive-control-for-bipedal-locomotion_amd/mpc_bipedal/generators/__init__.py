@@ -2,5 +2,6 @@
 
 from .footstep_generator import Contact, generate_footsteps
 from .cop_generator import CoPGenerator, State
+from .speed_generation import SpeedTrajectoryGenerator
 
-__all__ = ['Contact', 'generate_footsteps', 'CoPGenerator', 'State']
+__all__ = ['Contact', 'generate_footsteps', 'CoPGenerator', 'State', 'SpeedTrajectoryGenerator']

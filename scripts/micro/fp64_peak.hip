@@ -21,6 +21,23 @@ __global__ void __launch_bounds__(256) fma_chains(double* out, int iters, double
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+template <int CH>
+__global__ void __launch_bounds__(256) mfma_chains(double* out, int iters, double a0) {
+  dbl4 acc[CH];
+#pragma unroll
+  for (int c = 0; c < CH; ++c) acc[c] = dbl4{0.0, 0.0, 0.0, 0.0};
+  double a = a0 + threadIdx.x * 1e-6, b = 1.0 - threadIdx.x * 1e-7;
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int c = 0; c < CH; ++c) acc[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[c], 0, 0, 0);
+  }
+  double s = 0;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) s += acc[c][0] + acc[c][1] + acc[c][2] + acc[c][3];
+  out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
 template <int CW>
 __global__ void __launch_bounds__(128) corr_lds(const double* __restrict__ k, int kc, double* out, int reps) {
   __shared__ double z[64 * CW + 1024];
@@ -79,6 +96,20 @@ int main() {
     CHECK(hipEventElapsedTime(&ms, e0, e1));
     const double flops = 2.0 * 8 * iters * (double)blocks * 256;
     printf("fma_chains<8> waves/SIMD=%d: %.3f ms, %.1f TFLOP/s FP64\n", wpsimd, ms, flops / ms / 1e9);
+  }
+  for (int wpsimd : {1, 2, 4}) {
+    const int blocks = cus * wpsimd;
+    for (int rep = 0; rep < 2; ++rep) {
+      CHECK(hipEventRecord(e0));
+      hipLaunchKernelGGL(mfma_chains<4>, dim3(blocks), dim3(256), 0, 0, out, iters, 1e-3);
+      CHECK(hipEventRecord(e1));
+      CHECK(hipEventSynchronize(e1));
+    }
+    float ms;
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    const double flops = 2.0 * 1024 * 4 * iters * (double)blocks * 4;  // 4 waves per block
+    printf("mfma_f64_16x16x4 chains<4> waves/SIMD=%d: %.3f ms, %.1f TFLOP/s FP64, %.1f cycles/MFMA at 2.4 GHz\n",
+           wpsimd, ms, flops / ms / 1e9, ms * 1e-3 * 2.4e9 / (4.0 * iters * wpsimd));
   }
   const int kc = 154, reps = 200;
   for (int wpsimd : {2, 4, 8}) {

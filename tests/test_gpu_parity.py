@@ -118,6 +118,27 @@ def test_batched_step_vs_reference():
     assert int(st.abs().max()) == 0
 
 
+def test_speed_generator_wieber_vs_reference():
+    """SpeedTrajectoryGenerator wieber mode (speed_generation.py:55-67):
+    velocity rows of the reference's own zero-start state rollout (walk_n150 fixture), and
+    the batched form on the same walk."""
+    from mpc_bipedal.generators import SpeedTrajectoryGenerator
+    d = golden("walk_n150.npz")
+    dj = dict(ssp_duration=0.24, dsp_duration=0.03, standing_duration=1.0, distance=2.1,
+              step_length=0.3, foot_spread=0.1, horizon=150, Q=1.0, R=1e-6, S=1.0, h=0.75,
+              g=9.81, m=40.0, F_ext=400.0, strict=False, add_force=True,
+              speed_generation="wieber")
+    g = SpeedTrajectoryGenerator(MPCConfig(**dj))
+    vx, vy, st = g.generate_speed_and_state(save_footsteps=False)
+    assert np.abs(vx - d["state_x_hist"][:, 1, 0]).max() <= 1e-9
+    assert np.abs(vy - d["state_y_hist"][:, 1, 0]).max() <= 1e-9
+    bx, by = g.generate_speed_batch(np.repeat(d["zmax"][None], 3, 0),
+                                    np.repeat(d["zmin"][None], 3, 0))
+    assert bx.shape == (3, len(vx))
+    assert np.abs(bx.cpu().numpy() - vx[None]).max() <= 1e-12
+    assert np.abs(by.cpu().numpy() - vy[None]).max() <= 1e-12
+
+
 # --------------------------------------------------------------------------- batches
 
 

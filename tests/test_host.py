@@ -136,3 +136,21 @@ def test_product_has_no_oracle_or_cpu_solver_import():
                 src = open(os.path.join(dirpath, f)).read()
                 assert "oracle" not in src.replace("no oracle", ""), f
                 assert "linalg.inv" not in src and "linalg.solve" not in src, f
+
+
+def test_speed_generator_classic_and_errors():
+    """speed_generation.py:49-53 (classic: 0.3 m/s except STANDING) and :67 (unknown mode),
+    on the golden CoP state timeline."""
+    from mpc_bipedal.generators import SpeedTrajectoryGenerator, State
+    d = golden("cop_default_n150.npz")
+    cfg = MPCConfig(horizon=int(d["horizon"]), dt=float(d["dt"]), distance=float(d["distance"]),
+                    step_length=float(d["step_length"]), foot_spread=float(d["foot_spread"]),
+                    ssp_duration=float(d["ssp_duration"]), dsp_duration=float(d["dsp_duration"]),
+                    standing_duration=float(d["standing_duration"]), speed_generation="classic")
+    vx, vy, st = SpeedTrajectoryGenerator(cfg).generate_speed_and_state(save_footsteps=False)
+    standing = d["states"] == STATE_CODE[State.STANDING.value]
+    assert np.array_equal(vx, np.where(standing, 0.0, 0.3)) and not vy.any()
+    assert len(st) == len(d["states"])
+    bad = SpeedTrajectoryGenerator(MPCConfig(speed_generation="nope"))
+    with pytest.raises(ValueError, match="Unknown speed_generation mode"):
+        bad.generate_speed_and_state(save_footsteps=False)
