@@ -815,6 +815,216 @@ __global__ void __launch_bounds__(128, 4)
   }
 }
 
+// Long walks (64·8+1 < n ≤ 64·8·8+1): the split-axis structure widened to W waves per axis
+// (workgroup = 2·W waves; wave w of an axis owns timesteps [w·64·CW, (w+1)·64·CW)).  Each
+// wave scans its range from a zero state; the true start state of wave w is chained over the
+// waves' end states with M = (Ā^CW)^64 (plan level 6), and lane l adds (Ā^CW)^(l+1)·x_start by
+// binary powering.  History staged through the z_ref area in rounds (replay per round).
+template <int CW, int W>
+__global__ void __launch_bounds__(128 * W, 4) zmpc_rollout_unc_wide_kernel(RolloutArgs a) {
+  using ZL = ZrLayout<CW>;
+  constexpr int NT = 128 * W;
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  __shared__ int flag[2 * W];
+  __shared__ double send[2][W][3];  // zero-start end state of each wave (wave 0: true)
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int axis = wv / W, w = wv % W;
+  const int64_t b = blockIdx.x;
+  const int n = a.n, nsteps = n - 1;
+  double* zr0 = smem;
+  double* zr1 = zr0 + a.lzp;
+  // ---- 1. z_ref rows + window padding (zmp_controller.py:81-88) ----------------------------
+  {
+    const double2* zmx = reinterpret_cast<const double2*>(a.zmax + b * a.bstride);
+    const double2* zmn = reinterpret_cast<const double2*>(a.zmin + b * a.bstride);
+    for (int t0 = 0; t0 < a.lz; t0 += 4 * NT) {
+      double2 hi[4], lo[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int tc = (a.dbg & 8) ? 0 : min(t0 + u * NT + tid, n - 1);  // padding = last row
+        hi[u] = zmx[tc];
+        lo[u] = zmn[tc];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int t = t0 + u * NT + tid;
+        if (t < a.lz) {
+          zr0[ZL::idx(t)] = (hi[u].x + lo[u].x) / 2;
+          zr1[ZL::idx(t)] = (hi[u].y + lo[u].y) / 2;
+        }
+      }
+    }
+  }
+  const double* xb = a.x0 + b * 6 + 3 * axis;
+  const double xi[3] = {xb[0], xb[1], xb[2]};
+  const double kk = (axis == 1 && a.kick != nullptr) ? a.kick[b] : 0.0;
+  __syncthreads();
+  // ---- 2. correlation ------------------------------------------------------------------------
+  const int mbeg = (w * 64 + lane) * CW;
+  double f[CW];
+  axis_correlate<CW>(a, a.k, (axis ? zr1 : zr0) + ZL::idx(w * 64 * CW), lane, f);
+  // ---- 3. scan: per-wave zero-start Kogge-Stone, then the cross-wave offsets ---------------
+  const int64_t kick_step = (axis == 1) ? a.kick_step : -1;
+  const LipmConsts lc = a.lc;
+  const double kx0 = a.kx[0], kx1 = a.kx[1], kx2 = a.kx[2];
+  const double Bv[3] = {lc.T3_6, lc.T2_2, lc.T};
+  Mat3 Ab;
+  {
+    const double A[9] = {1.0, lc.T, lc.T2_2, 0.0, 1.0, lc.T, 0.0, 0.0, 1.0};
+    const double kx[3] = {kx0, kx1, kx2};
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) Ab.m[3 * i + j] = A[3 * i + j] - Bv[i] * kx[j];
+  }
+  double sv[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+  for (int q = 0; q < CW; ++q) {
+    if (mbeg + q < nsteps) {
+      double t[3];
+      matvec3(Ab, sv, t);
+      sv[0] = fma(Bv[0], f[q], t[0]);
+      sv[1] = fma(Bv[1], f[q], t[1]);
+      sv[2] = fma(Bv[2], f[q], t[2]);
+      if (mbeg + q == kick_step) sv[1] -= kk;
+    }
+  }
+  const double* Pp = a.scanP + (CW - 1) * kScanStride;  // (Ā^CW)^(2^r), r = 0..6
+  if (lane == 0 && w == 0) {
+    double t[3];
+    Mat3 P;
+#pragma unroll
+    for (int q = 0; q < 9; ++q) P.m[q] = Pp[q];
+    matvec3(P, xi, t);
+    for (int i = 0; i < 3; ++i) sv[i] += t[i];
+  }
+#pragma unroll
+  for (int r2 = 0; r2 < 6; ++r2) {
+    const int d = 1 << r2;
+    if (a.dbg & 2) break;
+    double u[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) u[i] = __shfl_up(sv[i], d, 64);
+    if (lane >= d) {
+      Mat3 Pd;
+#pragma unroll
+      for (int q = 0; q < 9; ++q) Pd.m[q] = Pp[r2 * 9 + q];
+      double t[3];
+      matvec3(Pd, u, t);
+      for (int i = 0; i < 3; ++i) sv[i] += t[i];
+    }
+  }
+  if (lane == 63) {
+    send[axis][w][0] = sv[0];
+    send[axis][w][1] = sv[1];
+    send[axis][w][2] = sv[2];
+  }
+  __syncthreads();  // end states published; z_ref dead (staging from here on)
+  double xs[3] = {xi[0], xi[1], xi[2]};  // this wave's start state
+  if (w > 0) {
+    Mat3 M64;
+#pragma unroll
+    for (int q = 0; q < 9; ++q) M64.m[q] = Pp[6 * 9 + q];
+    for (int i = 0; i < 3; ++i) xs[i] = send[axis][0][i];
+    for (int v = 1; v < w; ++v) {
+      double t[3];
+      matvec3(M64, xs, t);
+      for (int i = 0; i < 3; ++i) xs[i] = send[axis][v][i] + t[i];
+    }
+    double vv[3] = {xs[0], xs[1], xs[2]};
+    const int e = lane + 1;
+#pragma unroll
+    for (int r2 = 0; r2 < 7; ++r2) {
+      if ((e >> r2) & 1) {
+        Mat3 Pd;
+#pragma unroll
+        for (int q = 0; q < 9; ++q) Pd.m[q] = Pp[r2 * 9 + q];
+        double t[3];
+        matvec3(Pd, vv, t);
+        for (int i = 0; i < 3; ++i) vv[i] = t[i];
+      }
+    }
+    for (int i = 0; i < 3; ++i) sv[i] += vv[i];
+  }
+  double xs0[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const double p = __shfl_up(sv[i], 1, 64);
+    xs0[i] = (lane == 0) ? xs[i] : p;
+  }
+  // ---- 4. replay (reference form) into the staging rows, coalesced copy-out per round --------
+  double* stage = smem;
+  const int rows_per_round = (2 * a.lzp) / 6;
+  double* hb = a.hist + b * (int64_t)n * 6;
+  double x[3];
+  for (int r0 = 0; r0 < n; r0 += rows_per_round) {
+    const int r1 = min(r0 + rows_per_round, n);
+    if (lane == 0 && w == 0 && r0 == 0) {
+      stage[3 * axis + 0] = xi[0];
+      stage[3 * axis + 1] = xi[1];
+      stage[3 * axis + 2] = xi[2];
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) x[i] = xs0[i];
+#pragma unroll
+    for (int q = 0; q < CW; ++q) {
+      const int m = mbeg + q;
+      if (m < nsteps) {
+        const double u = f[q] - (kx0 * x[0] + kx1 * x[1] + kx2 * x[2]);
+        double xn[3];
+        lipm_step(lc, x, u, xn);
+        if (m == kick_step) xn[1] -= kk;
+        const int row = m + 1;
+        if (row >= r0 && row < r1) {
+          double* o = stage + (row - r0) * 6 + 3 * axis;
+          o[0] = xn[0];
+          o[1] = xn[1];
+          o[2] = xn[2];
+        }
+#pragma unroll
+        for (int i = 0; i < 3; ++i) x[i] = xn[i];
+      }
+    }
+    __syncthreads();
+    if (!(a.dbg & 4)) {
+      const int nd2 = (r1 - r0) * 3;
+      const double2* src = reinterpret_cast<const double2*>(stage);
+      double2* dst = reinterpret_cast<double2*>(hb + (int64_t)r0 * 6);
+      for (int e = tid; e < nd2; e += NT) dst[e] = src[e];
+    }
+    __syncthreads();
+  }
+  if (a.status != nullptr) {
+    const bool finite = isfinite(x[0]) && isfinite(x[1]) && isfinite(x[2]);
+    const unsigned long long bad = __ballot(!finite);
+    if (lane == 0) flag[wv] = bad ? ZMPC_ST_NONFINITE : 0;
+    __syncthreads();
+    if (tid == 0) {
+      int fl = 0;
+      for (int v = 0; v < 2 * W; ++v) fl |= flag[v];
+      a.status[b] = fl;
+    }
+  }
+}
+
+// Geometry of the wide kernel: W waves per axis (2, 4 or 8), CW = ceil((n−1)/(64·W)) ≤ 8.
+struct WideGeom {
+  int w, cw, kc, lz, lzp;
+};
+
+bool wide_geom(int N, int64_t n, WideGeom* g) {
+  const int64_t ns = n - 1;
+  if (ns <= 64 * 8 || ns > 64 * 8 * 8) return false;
+  g->w = ns <= 64 * 8 * 2 ? 2 : (ns <= 64 * 8 * 4 ? 4 : 8);
+  g->cw = (int)((ns + 64 * g->w - 1) / (64 * g->w));
+  g->kc = (N + g->cw - 1) / g->cw * g->cw;
+  g->lz = g->w * 64 * g->cw + g->kc + 1;
+  const int pad = (g->cw % 2 == 0) ? 1 : 0;
+  g->lzp = ((g->lz + pad * (g->lz / g->cw) + 1) + 1) & ~1;
+  // default 64 KiB LDS cap (the 4-waves-per-SIMD bound leaves no room above it)
+  return (size_t)2 * g->lzp * sizeof(double) <= 64 * 1024;
+}
+
 // Longer walks (several correlation passes): one walk per wave, f through LDS.
 template <int CW>
 __global__ void __launch_bounds__(64) zmpc_rollout_unc_long_kernel(RolloutArgs a) {
@@ -982,6 +1192,29 @@ hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, con
   RolloutArgs a{g.kc, g.kcp, g.lz,      g.lzp, (int)n,     B,   p->lc,
                 p->k, p->kx,  zmax,      zmin,  bstride,    x0,  kick,
                 kick_step,    hist, status, p->scanP, dbg, 0};
+  WideGeom wg;
+  static const bool no_wide = getenv("ZMPC_ROLLOUT_NO_WIDE") != nullptr;  // A/B: long kernel
+  if (!no_wide && g.passes > 1 && wide_geom(p->N, n, &wg)) {
+    RolloutArgs q = a;
+    q.kc = wg.kc;
+    q.lz = wg.lz;
+    q.lzp = wg.lzp;
+    const size_t lds_w = 2 * (size_t)wg.lzp * sizeof(double);
+    switch (wg.w * 16 + wg.cw) {
+#define ZMPC_WCASE(W, C)                                                                      \
+  case W * 16 + C:                                                                            \
+    hipLaunchKernelGGL((zmpc_rollout_unc_wide_kernel<C, W>), dim3((unsigned)B), dim3(128 * W), \
+                       lds_w, s, q);                                                          \
+    break;
+      ZMPC_WCASE(2, 5) ZMPC_WCASE(2, 6) ZMPC_WCASE(2, 7) ZMPC_WCASE(2, 8)
+      ZMPC_WCASE(4, 5) ZMPC_WCASE(4, 6) ZMPC_WCASE(4, 7) ZMPC_WCASE(4, 8)
+      ZMPC_WCASE(8, 5) ZMPC_WCASE(8, 6) ZMPC_WCASE(8, 7) ZMPC_WCASE(8, 8)
+#undef ZMPC_WCASE
+      default:
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
   switch (g.cw) {
 #define ZMPC_CW(C)               \
   case C:                        \

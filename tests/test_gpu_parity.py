@@ -182,10 +182,10 @@ def test_shared_cop_equals_dense():
     assert torch.equal(h_shared, h_dense)
 
 
-@pytest.mark.parametrize("n", (1, 2, 3, 65, 130, 513, 700))
+@pytest.mark.parametrize("n", (1, 2, 3, 65, 130, 513, 514, 700, 1100, 2500, 4097))
 def test_walk_lengths(n):
-    """Ragged lengths: n=1 (no solve), chunk boundaries of the lane scan and of the
-    correlation passes."""
+    """Ragged lengths: n=1 (no solve), chunk boundaries of the lane scan, the single-pass /
+    wide (2, 4, 8 waves per axis) kernel boundaries (513 | 514, 1025, 2049, 4097)."""
     rng = np.random.default_rng(n)
     N = 40
     dt = 1.5 / N
