@@ -56,6 +56,8 @@ struct StrictArgs {
   int32_t* status;       // [B] or null
   double* scratch;       // per-wave N*N factor scratch (gridDim*SWAVES slots)
   unsigned long long* dbg;  // diagnostic phase counters (ZMPC_DEBUG_STRICT), null normally
+  int lds_chol;          // A/B: 1 = LDS Cholesky for every reduced size (ZMPC_STRICT_LDS_CHOL)
+  int gsz;               // doubles of LDS holding G packed (0: G read from L2)
 };
 
 // Diagnostic phase timer: only when a.dbg is set (a separate, opt-in run; never in the bench).
@@ -207,40 +209,50 @@ __device__ void wave_chol_solve(const Tri<PACKED>& T, double* v, int lane) {
 }
 
 struct WaveWork {
-  double* zs;    // [Np] D = unconstrained δ*
   double* zz;    // [Np] current δ
-  double* lo;    // [Np] z_min − c
-  double* hi;    // [Np] z_max − c
   double* nuf;   // [Np] multipliers scattered to horizon slots
   double* nuc;   // [Np] compact right-hand side / solution
+  double* rj;    // [Np] per-slot scratch read across lanes (dual rhs, primal W − H t)
   int* ia;       // [Np] compact active slots
   int* iff;      // [Np] compact free slots
-  double* S;     // packed LDS factor workspace (pcap doubles)
+  double* S;     // LDS factor workspace (pcap doubles)
   double* Sg;    // [N*N] global factor scratch
+  const double* Gs;  // G packed lower-triangular in LDS (N(N+1)/2), or null (G from L2)
 };
 
+__device__ __forceinline__ int tri_at(int i, int j) { return ((i * (i + 1)) >> 1) + j; }
+
+// G(r, c) from the LDS copy (symmetric, packed lower) or from global memory.
+__device__ __forceinline__ double g_at(const StrictArgs& a, const WaveWork& w, int r, int c) {
+  if (w.Gs) return w.Gs[r >= c ? tri_at(r, c) : tri_at(c, r)];
+  return a.G[(size_t)r * a.N + c];
+}
+
 // acc[c] −= Σ_r M[idx[r]][j_c] · coef[r] for the lane's horizon slots j_c = lane + 64c:
-// one coalesced row load per (r, c); four rows in flight per round.
+// one coalesced row load per (r, c); four rows in flight per round.  (Global M.)
 template <int NJ>
 __device__ __forceinline__ void row_combine(const double* M, int N, const int* idx,
                                             const double* coef, int count, double* acc,
                                             int lane) {
+  // RB rows (RB·NJ loads) in flight per round: the rows come from L2 at ~2k-cycle latency
+  // and one wave per SIMD has nothing else to hide it with
+  constexpr int RB = (NJ <= 3) ? 8 : 4;
   int r0 = 0;
-  for (; r0 + 4 <= count; r0 += 4) {
-    double g[4][NJ];
-    double cf[4];
+  for (; r0 + RB <= count; r0 += RB) {
+    double g[RB][NJ];
+    double cf[RB];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
+    for (int u = 0; u < RB; ++u) {
       const double* row = M + (size_t)idx[r0 + u] * N;
       cf[u] = coef[r0 + u];
 #pragma unroll
       for (int c = 0; c < NJ; ++c) {
         const int j = lane + 64 * c;
-        g[u][c] = (j < N) ? row[j] : 0.0;
+        g[u][c] = row[j < N ? j : 0];
       }
     }
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < RB; ++u)
 #pragma unroll
       for (int c = 0; c < NJ; ++c) acc[c] = fma(-g[u][c], cf[u], acc[c]);
   }
@@ -251,6 +263,22 @@ __device__ __forceinline__ void row_combine(const double* M, int N, const int* i
     for (int c = 0; c < NJ; ++c) {
       const int j = lane + 64 * c;
       if (j < N) acc[c] = fma(-row[j], cf, acc[c]);
+    }
+  }
+}
+
+// The same with G's packed LDS copy (rows of a symmetric matrix: G[r][j] = Gs[tri(max, min)]).
+template <int NJ>
+__device__ __forceinline__ void row_combine_lds(const double* Gs, int N, const int* idx,
+                                                const double* coef, int count, double* acc,
+                                                int lane) {
+  for (int r = 0; r < count; ++r) {
+    const int ir = idx[r];
+    const double cf = coef[r];
+#pragma unroll
+    for (int c = 0; c < NJ; ++c) {
+      const int j = lane + 64 * c;
+      if (j < N) acc[c] = fma(-Gs[j <= ir ? tri_at(ir, j) : tri_at(j, ir)], cf, acc[c]);
     }
   }
 }
@@ -279,12 +307,83 @@ __device__ __forceinline__ void gather_packed(const Tri<true>& T, Gather gather,
   }
 }
 
-// Factor the reduced matrix gathered by `gather(r, c)` (size m) and solve in place on w.nuc.
+// ---- register-resident reduced solve (m <= 64) ------------------------------------------
+// Lane i < m owns row i of the trailing matrix: at column step k, a[j] = element (i, k + j)
+// (the array shifts one slot per column, so every register index is static in a rolled
+// k-loop).  Column k is broadcast with v_readlane (wave-uniform lane index): a column costs
+// MR FMAs + 2·MR readlanes per lane and no memory round trip.  The inner loops carry no
+// guards (MR is the smallest of 16/32/48/64 covering m; entries past m stay 0), so they are
+// straight-line code.  L's rows go to LDS (packed) for the two triangular solves, which chain
+// through v_readlane.
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, l);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// Solve M_II y = rhs, M_II[r][c] = gather(r, c) (symmetric positive definite, r >= c asked),
+// rhs in LDS (overwritten with y), Ls = LDS scratch of m(m+1)/2 doubles.  False if a pivot is
+// not positive.
+template <int MR, class Gather>
+__device__ __noinline__ bool reg_chol_solve(Gather gather, int m, double* rhs, double* Ls, int lane) {
+  double a[MR];
+#pragma unroll
+  for (int j = 0; j < MR; ++j) a[j] = (j < m && lane < m && j <= lane) ? gather(lane, j) : 0.0;
+  double invd = 0.0;
+  for (int k = 0; k < m; ++k) {
+    const double d = readlane_d(a[0], k);
+    if (!(d > 0.0)) return false;
+    const double piv = sqrt(d);
+    const double inv = 1.0 / piv;
+    const double l = (lane == k) ? piv : ((lane > k && lane < m) ? a[0] * inv : 0.0);
+    if (lane == k) invd = inv;
+    if (lane >= k && lane < m) Ls[tri_at(lane, k)] = l;
+#pragma unroll
+    for (int j = 1; j < MR; ++j) a[j - 1] = fma(-l, readlane_d(l, (k + j) & 63), a[j]);
+    a[MR - 1] = 0.0;
+  }
+  lds_sync();
+  // forward L y = rhs
+  double acc = (lane < m) ? rhs[lane] : 0.0;
+  double y = 0.0;
+  for (int j = 0; j < m; ++j) {
+    const double lij = (lane > j && lane < m) ? Ls[tri_at(lane, j)] : 0.0;
+    const double yj = readlane_d(acc * invd, j);
+    if (lane == j) y = yj;
+    acc = fma(-lij, yj, acc);
+  }
+  // backward Lᵀ x = y (column j of Lᵀ = row j of L)
+  acc = y;
+  double x = 0.0;
+  for (int j = m - 1; j >= 0; --j) {
+    const double lji = (lane < j) ? Ls[tri_at(j, lane)] : 0.0;
+    const double xj = readlane_d(acc * invd, j);
+    if (lane == j) x = xj;
+    acc = fma(-lji, xj, acc);
+  }
+  lds_sync();
+  if (lane < m) rhs[lane] = x;
+  lds_sync();
+  return true;
+}
+
+// Factor the reduced matrix gathered by `gather(r, c)` (size m) and solve in place on w.nuc:
+// registers for m <= 32, the packed LDS factor while it fits, else the wave's global scratch.
 template <class Gather>
-__device__ bool reduced_solve(const StrictArgs& a, const WaveWork& w, int m, Gather gather,
+__device__ __forceinline__ bool reduced_solve(const StrictArgs& a, const WaveWork& w, int m, Gather gather,
                               int lane) {
   PhaseClock clk(a.dbg);
   clk.count(12, m, lane);
+  clk.count(m <= 16 ? 16 : m <= 32 ? 17 : m <= 48 ? 18 : m <= 64 ? 19 : 20, 1, lane);
+  if (m <= 64 && m * (m + 1) / 2 <= a.pcap && !a.lds_chol) {
+    const bool ok = m <= 16   ? reg_chol_solve<16>(gather, m, w.nuc, w.S, lane)
+                    : m <= 32 ? reg_chol_solve<32>(gather, m, w.nuc, w.S, lane)
+                    : m <= 48 ? reg_chol_solve<48>(gather, m, w.nuc, w.S, lane)
+                              : reg_chol_solve<64>(gather, m, w.nuc, w.S, lane);
+    clk.lap(3, lane);
+    return ok;
+  }
   if (m * (m + 1) / 2 <= a.pcap && m <= 128) {
     Tri<true> T{w.S, m};
     gather_packed(T, gather, lane);
@@ -310,33 +409,34 @@ __device__ bool reduced_solve(const StrictArgs& a, const WaveWork& w, int m, Gat
 
 // One strict QP solve for one instance.  D holds G·W on entry; st is the instance's
 // warm-start status array (0 free, 1 upper, 2 lower), updated in place.  Returns u0 and
-// ORs failure flags into *flags.
+// ORs failure flags into *flags.  The lane's own horizon slots (j = lane + 64c) keep D and
+// the shifted bounds in registers; only what other lanes read goes through LDS.
 template <int NJ>
-__device__ double solve_instance(const StrictArgs& a, int64_t inst, int64_t i, const double* x,
+__device__ __forceinline__ double solve_instance(const StrictArgs& a, int64_t inst, int64_t i, const double* x,
                                  const double* D, signed char* st, const WaveWork& w, int lane,
                                  int* flags) {
   const int N = a.N;
   PhaseClock clk(a.dbg);
+  double zs[NJ], hi[NJ], lo[NJ];  // D, z_max − c, z_min − c on the lane's slots
   {
-    double hi[NJ], lo[NJ];
+    double bh[NJ], bl[NJ];
 #pragma unroll
     for (int c = 0; c < NJ; ++c) {
       const int j = lane + 64 * c;
-      if (j < N) {
-        const int64_t e = bound_index(a, inst, i, j);
-        hi[c] = a.zmax[e];
-        lo[c] = a.zmin[e];
-      }
+      const int64_t e = bound_index(a, inst, i, j < N ? j : N - 1);
+      bh[c] = a.zmax[e];
+      bl[c] = a.zmin[e];
     }
 #pragma unroll
     for (int c = 0; c < NJ; ++c) {
       const int j = lane + 64 * c;
+      zs[c] = hi[c] = lo[c] = 0.0;
       if (j < N) {
         const double cj = px_dot(a, j, x);
-        w.hi[j] = hi[c] - cj;
-        w.lo[j] = lo[c] - cj;
-        w.zs[j] = D[j];
-        w.zz[j] = D[j];
+        hi[c] = bh[c] - cj;
+        lo[c] = bl[c] - cj;
+        zs[c] = D[j];
+        w.zz[j] = zs[c];
         w.nuf[j] = 0.0;
       }
     }
@@ -371,20 +471,22 @@ __device__ double solve_instance(const StrictArgs& a, int64_t inst, int64_t i, c
       for (int c = 0; c < NJ; ++c) {
         const int j = lane + 64 * c;
         if (j < N) {
-          w.zz[j] = w.zs[j];
+          w.zz[j] = zs[c];
           w.nuf[j] = 0.0;
         }
       }
     } else if (m <= f) {
       // dual: G_AA ν = D_A − t_A
-      for (int r = lane; r < m; r += 64) {
-        const int j = w.ia[r];
-        w.nuc[r] = w.zs[j] - (st[j] == 1 ? w.hi[j] : w.lo[j]);
+#pragma unroll
+      for (int c = 0; c < NJ; ++c) {
+        const int j = lane + 64 * c;
+        if (j < N && st[j] != 0) w.rj[j] = zs[c] - (st[j] == 1 ? hi[c] : lo[c]);
       }
       lds_sync();
+      for (int r = lane; r < m; r += 64) w.nuc[r] = w.rj[w.ia[r]];
+      lds_sync();
       const int* ia = w.ia;
-      const double* G = a.G;
-      if (!reduced_solve(a, w, m, [&](int r, int c) { return G[(size_t)ia[r] * N + ia[c]]; },
+      if (!reduced_solve(a, w, m, [&](int r, int c) { return g_at(a, w, ia[r], ia[c]); },
                          lane)) {
         *flags |= ZMPC_ST_FACTOR;
         break;
@@ -394,12 +496,15 @@ __device__ double solve_instance(const StrictArgs& a, int64_t inst, int64_t i, c
 #pragma unroll
       for (int c = 0; c < NJ; ++c) {
         const int j = lane + 64 * c;
-        acc[c] = (j < N) ? w.zs[j] : 0.0;
+        acc[c] = zs[c];
         if (j < N) w.nuf[j] = 0.0;
       }
       lds_sync();
       for (int r = lane; r < m; r += 64) w.nuf[w.ia[r]] = w.nuc[r];
-      row_combine<NJ>(a.G, N, w.ia, w.nuc, m, acc, lane);
+      if (w.Gs)
+        row_combine_lds<NJ>(w.Gs, N, w.ia, w.nuc, m, acc, lane);
+      else
+        row_combine<NJ>(a.G, N, w.ia, w.nuc, m, acc, lane);
 #pragma unroll
       for (int c = 0; c < NJ; ++c) {
         const int j = lane + 64 * c;
@@ -412,20 +517,22 @@ __device__ double solve_instance(const StrictArgs& a, int64_t inst, int64_t i, c
       for (int c = 0; c < NJ; ++c) {
         const int j = lane + 64 * c;
         y[c] = 0.0;
-        if (j < N) w.zz[j] = (st[j] == 1) ? w.hi[j] : ((st[j] == 2) ? w.lo[j] : 0.0);
+        if (j < N) w.zz[j] = (st[j] == 1) ? hi[c] : ((st[j] == 2) ? lo[c] : 0.0);
       }
       lds_sync();
       for (int r = lane; r < m; r += 64) w.nuc[r] = -w.zz[w.ia[r]];
       lds_sync();
       row_combine<NJ>(a.Hz, N, w.ia, w.nuc, m, y, lane);  // y = H t_A (scattered)
-      // W_j − y_j for every slot, kept in nuf for now
+      // W_j − y_j for every slot (W = Q (z_ref − c) = Q (hi + lo) / 2)
+      double wy[NJ];
 #pragma unroll
       for (int c = 0; c < NJ; ++c) {
         const int j = lane + 64 * c;
-        if (j < N) w.nuf[j] = a.Q * ((w.hi[j] + w.lo[j]) / 2) - y[c];
+        wy[c] = a.Q * ((hi[c] + lo[c]) / 2) - y[c];
+        if (j < N) w.rj[j] = wy[c];
       }
       lds_sync();
-      for (int r = lane; r < f; r += 64) w.nuc[r] = w.nuf[w.iff[r]];
+      for (int r = lane; r < f; r += 64) w.nuc[r] = w.rj[w.iff[r]];
       lds_sync();
       const int* iff = w.iff;
       const double* H = a.Hz;
@@ -446,7 +553,7 @@ __device__ double solve_instance(const StrictArgs& a, int64_t inst, int64_t i, c
 #pragma unroll
       for (int c = 0; c < NJ; ++c) {
         const int j = lane + 64 * c;
-        if (j < N) w.nuf[j] = (st[j] != 0) ? (w.nuf[j] - v2[c]) : 0.0;
+        if (j < N) w.nuf[j] = (st[j] != 0) ? (wy[c] - v2[c]) : 0.0;
       }
     }
     lds_sync();
@@ -462,13 +569,14 @@ __device__ double solve_instance(const StrictArgs& a, int64_t inst, int64_t i, c
       if (j < N) {
         const signed char o = st[j];
         signed char v = o;
+        const double zj = w.zz[j], nj = w.nuf[j];
         if (o == 1) {
-          if (w.nuf[j] < -tolnu) v = 0;
+          if (nj < -tolnu) v = 0;
         } else if (o == 2) {
-          if (w.nuf[j] > tolnu) v = 0;
-        } else if (w.zz[j] > w.hi[j] + tolz) {
+          if (nj > tolnu) v = 0;
+        } else if (zj > hi[c] + tolz) {
           v = 1;
-        } else if (w.zz[j] < w.lo[j] - tolz) {
+        } else if (zj < lo[c] - tolz) {
           v = 2;
         }
         ns[c] = v;
@@ -549,25 +657,34 @@ __global__ void __launch_bounds__(256) zmpc_strict_kernel(StrictArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int Np = a.Np, ld = a.ld;
-  // LDS carve: Wt [SNB][ld] | xs [SNB][4] | flags [SNB] (as doubles) |
-  //            per wave {zs,zz,lo,hi,nuf,nuc}[Np], ia/iff[Np] ints, S[pcap] | st [SNB][Np] B
-  double* Wt = smem;
+  // LDS carve: Gs [gsz] (G packed lower, when it fits) | Wt [SNB][ld] | xs [SNB][4] |
+  //            flags [SNB] (as doubles) | per wave {zz,nuf,nuc,rj}[Np], ia/iff[Np] ints,
+  //            S[pcap] | st [SNB][Np] B
+  double* Gs = smem;
+  double* Wt = Gs + a.gsz;
   double* xs = Wt + SNB * ld;
   int* fl = reinterpret_cast<int*>(xs + SNB * 4);
   double* wbase = xs + SNB * 4 + SNB;
-  const int per_wave = 7 * Np + a.pcap;
+  const int per_wave = 5 * Np + a.pcap;
   double* my = wbase + wave * per_wave;
   WaveWork w;
-  w.zs = my;
-  w.zz = my + Np;
-  w.lo = my + 2 * Np;
-  w.hi = my + 3 * Np;
-  w.nuf = my + 4 * Np;
-  w.nuc = my + 5 * Np;
-  w.ia = reinterpret_cast<int*>(my + 6 * Np);
+  w.zz = my;
+  w.nuf = my + Np;
+  w.nuc = my + 2 * Np;
+  w.rj = my + 3 * Np;
+  w.ia = reinterpret_cast<int*>(my + 4 * Np);
   w.iff = w.ia + Np;
-  w.S = my + 7 * Np;
+  w.S = my + 5 * Np;
   w.Sg = a.scratch + ((size_t)blockIdx.x * SWAVES + wave) * (size_t)a.N * a.N;
+  w.Gs = nullptr;
+  if (a.gsz > 0) {
+    // G (symmetric, batch-invariant) packed into LDS once per workgroup: every reduced-matrix
+    // gather and row combination of the active-set solves then reads LDS, not L2
+    for (int r = wave; r < a.N; r += SWAVES)
+      for (int c = lane; c <= r; c += 64) Gs[tri_at(r, c)] = a.G[(size_t)r * a.N + c];
+    w.Gs = Gs;
+    __syncthreads();
+  }
   signed char* stall = reinterpret_cast<signed char*>(wbase + SWAVES * per_wave);
 
   const int64_t ntiles = (a.ninst + SNB - 1) / SNB;
@@ -677,9 +794,10 @@ __global__ void __launch_bounds__(256) zmpc_strict_kernel(StrictArgs a) {
   }
 }
 
-size_t strict_lds_bytes(int Np, int ld, int pcap) {
-  const size_t per_wave = 7 * Np + (size_t)pcap;
-  return (SNB * ld + SNB * 4 + SNB + SWAVES * per_wave) * sizeof(double) + SNB * Np;
+size_t strict_lds_bytes(int Np, int ld, int pcap, int gsz) {
+  const size_t per_wave = 5 * Np + (size_t)pcap;
+  return ((size_t)gsz + SNB * ld + SNB * 4 + SNB + SWAVES * per_wave) * sizeof(double) +
+         SNB * Np;
 }
 
 }  // namespace
@@ -705,15 +823,21 @@ static hipError_t launch_strict(const zmpc_plan* p, StrictArgs a, hipStream_t s,
   a.N = p->N;
   a.Np = (p->N + 15) & ~15;
   a.ld = a.Np + 4;
-  // packed factor room for min(|A|, |F|) <= N/2 when it fits, else as much as fits
   const size_t budget = 160 * 1024 - 512;
-  if (strict_lds_bytes(a.Np, a.ld, 0) > budget) {
+  if (strict_lds_bytes(a.Np, a.ld, 0, 0) > budget) {
     *why = "horizon too long for the strict solver's LDS tile (N=" + std::to_string(p->N) + ")";
     return hipErrorInvalidValue;
   }
+  // G packed in LDS when it fits beside a factor room for m <= 32 — N <= ~150; the rest of
+  // the room then holds the packed factor
+  // (A/B only: measured slower at N = 150 — the factor room it leaves is too small)
+  static const bool lds_g = getenv("ZMPC_STRICT_LDS_G") != nullptr;
+  const int gsz = ((p->N * (p->N + 1) / 2) + 1) & ~1;
+  a.gsz = (lds_g && strict_lds_bytes(a.Np, a.ld, 32 * 33 / 2, gsz) <= budget) ? gsz : 0;
+  // packed factor room for min(|A|, |F|) <= N/2 when it fits, else as much as fits
   const int half = p->N / 2;
   int pcap = half * (half + 1) / 2;
-  const size_t fixed = strict_lds_bytes(a.Np, a.ld, 0);
+  const size_t fixed = strict_lds_bytes(a.Np, a.ld, 0, a.gsz);
   const int fit = (int)((budget - fixed) / (SWAVES * sizeof(double)));
   if (pcap > fit) pcap = fit;
   a.pcap = pcap & ~1;
@@ -727,7 +851,9 @@ static hipError_t launch_strict(const zmpc_plan* p, StrictArgs a, hipStream_t s,
   const int64_t ntiles = (a.ninst + SNB - 1) / SNB;
   int grid = (int)std::min<int64_t>(ntiles, (int64_t)p->strict_slots);
   a.scratch = p->scratch;
-  const size_t lds = strict_lds_bytes(a.Np, a.ld, a.pcap);
+  const size_t lds = strict_lds_bytes(a.Np, a.ld, a.pcap, a.gsz);
+  static const bool lds_chol = getenv("ZMPC_STRICT_LDS_CHOL") != nullptr;  // A/B only
+  a.lds_chol = lds_chol ? 1 : 0;
   static const bool dbg_on = getenv("ZMPC_DEBUG_STRICT") != nullptr;  // diagnostics only
   static unsigned long long* dbgbuf = nullptr;
   if (dbg_on && !dbgbuf) (void)hipMalloc((void**)&dbgbuf, 32 * sizeof(unsigned long long));
@@ -760,6 +886,8 @@ static hipError_t launch_strict(const zmpc_plan* p, StrictArgs a, hipStream_t s,
             "global_fact=%llu\n",
             grid, a.pcap, h[0], h[1], h[2], h[3], h[4], h[5], h[6], h[7], h[8], h[15], h[11],
             h[9], h[10], h[13], h[12], h[14]);
+    fprintf(stderr, "[zmpc strict dbg] reduced sizes: <=16 %llu, 17-32 %llu, 33-48 %llu, "
+            "49-64 %llu, >64 %llu; gsz=%d\n", h[16], h[17], h[18], h[19], h[20], a.gsz);
   }
   return e;
 }

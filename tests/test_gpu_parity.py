@@ -139,6 +139,30 @@ def test_speed_generator_wieber_vs_reference():
     assert np.abs(by.cpu().numpy() - vy[None]).max() <= 1e-12
 
 
+def test_cli_matches_reference_walk(tmp_path):
+    """mpc_bipedal.cli (run_mpc.py semantics) on default.json, unconstrained: the saved CoM
+    equals the reference walk; --batch sweeps F_ext over [0, 2·F_ext] in one rollout
+    (the middle walk of an odd batch is the F_ext walk)."""
+    import json
+    from mpc_bipedal import cli
+    d = golden("walk_n150.npz")
+    cfgf = tmp_path / "default.json"
+    cfgf.write_text(json.dumps({"mpc": dict(
+        ssp_duration=0.24, dsp_duration=0.03, standing_duration=1.0, distance=2.1,
+        step_length=0.3, foot_spread=0.1, horizon=150, Q=1.0, R=1e-6, S=1.0, h=0.75, g=9.81,
+        m=40.0, F_ext=400.0, strict=True, add_force=True)}))
+    out = tmp_path / "o.npz"
+    assert cli.main(["--config", str(cfgf), "--no-strict", "--save", str(out)]) == 0
+    r = np.load(out)
+    assert rmse(r["com"][0], d["com_force"]) <= 1e-9
+    out3 = tmp_path / "o3.npz"
+    assert cli.main(["--config", str(cfgf), "--no-strict", "--batch", "3", "--save",
+                     str(out3)]) == 0
+    r3 = np.load(out3)
+    assert r3["com"].shape == (3,) + d["com_force"].shape
+    assert rmse(r3["com"][1], d["com_force"]) <= 1e-9
+
+
 # --------------------------------------------------------------------------- batches
 
 

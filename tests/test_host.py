@@ -154,3 +154,23 @@ def test_speed_generator_classic_and_errors():
     bad = SpeedTrajectoryGenerator(MPCConfig(speed_generation="nope"))
     with pytest.raises(ValueError, match="Unknown speed_generation mode"):
         bad.generate_speed_and_state(save_footsteps=False)
+
+
+def test_cli_config_semantics(tmp_path):
+    """run_mpc.py:23-40,153-221 semantics in mpc_bipedal.cli: only the
+    "mpc" section is read, a lone dt sets horizon = int(1.5/dt), dt is always 1.5/horizon,
+    flags override the file, --no-strict / --no-add-force."""
+    import json
+    from mpc_bipedal import cli
+    f = tmp_path / "c.json"
+    f.write_text(json.dumps({"cop_generator": {"distance": 9.9},
+                             "mpc": {"dt": 0.02, "Q": 2.0, "strict": True}}))
+    c = cli.config_from_args(cli.build_parser().parse_args(["--config", str(f)]))
+    assert c.horizon == 75 and c.dt == 1.5 / 75 and c.Q == 2.0 and c.distance == 2.1
+    c = cli.config_from_args(cli.build_parser().parse_args(
+        ["--config", str(f), "--horizon", "64", "--no-strict", "--no-add-force", "--F-ext", "7",
+         "--distance", "3.0"]))
+    assert c.horizon == 64 and c.dt == 1.5 / 64 and not c.strict and not c.add_force
+    assert c.F_ext == 7.0 and c.distance == 3.0 and c.backend == "hip"
+    c = cli.config_from_args(cli.build_parser().parse_args(["--config", str(f), "--dt", "0.05"]))
+    assert c.horizon == 30 and c.dt == 1.5 / 30
