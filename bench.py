@@ -232,19 +232,22 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
+    # one HIP event pair brackets the K back-to-back launches on their stream: kernel_ms is
+    # the average launch duration (per-launch event pairs would add a marker packet, and an
+    # idle gap, between consecutive kernels)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    ev0.record(stream)
     for k in range(args.steps):
-        ev[k][0].record(stream)
         launch()
-        ev[k][1].record(stream)
+    ev1.record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -282,6 +285,29 @@ def main():
         torch.cuda.synchronize()
         gather_ms = (time.perf_counter() - tg) * 1e3
         assert full.shape[0] == B * world
+
+    # batches pipelined two-deep on two streams (separate history buffers): consecutive
+    # rollouts overlap, so one's memory phases run under the other's FP64 phases — what a
+    # many-batch driver gets; reported beside `value`, not as it
+    pipelined = None
+    if rank == 0 and world == 1 and not cfg.strict:
+        streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
+        hist2 = torch.empty_like(hist)
+        with torch.cuda.stream(streams[1]):
+            launch2 = plan.rollout_launcher(zmax, zmin, x0, kick=kick, kick_step=kstep,
+                                            hist=hist2)
+        launches = [launch, launch2]
+        torch.cuda.synchronize()
+        tq = time.perf_counter()
+        for k in range(args.steps):
+            with torch.cuda.stream(streams[k % 2]):
+                launches[k % 2]()
+        torch.cuda.synchronize()
+        tq = (time.perf_counter() - tq) / args.steps
+        assert torch.equal(hist, hist2)
+        pipelined = {"value": B * (n - 1) * 2 / tq, "unit": "QP solves/s",
+                     "ms_per_step": tq * 1e3, "streams": 2,
+                     "hbm_gbs_aggregate": alg_bytes / tq / 1e9}
 
     # the drop-in batch API hands host arrays over: PCIe-inclusive rate (never `value`)
     pcie = None
@@ -355,6 +381,7 @@ def main():
             "com_rmse_vs_ref": com_rmse_ref,
             "allgather_ms": gather_ms,
             "pcie_inclusive": pcie,
+            "pipelined": pipelined,
         }
         print(json.dumps(line))
     if world > 1:
