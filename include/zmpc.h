@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define ZMPC_ABI_VERSION 1
+#define ZMPC_ABI_VERSION 2
 
 /* return codes */
 #define ZMPC_OK 0
@@ -101,6 +101,33 @@ int zmpc_rollout(const zmpc_plan* plan, int64_t B, int64_t n, const double* zmax
                  const double* zmin, int64_t bounds_stride, const double* x0,
                  const double* kick, int64_t kick_step, double* hist, int32_t* status,
                  void* stream);
+
+/*
+ * zmpc_rollout with a kick step per walk (ragged batches: the reference applies the force at
+ * step n_b//2 of each walk, zmp_controller.py:90).  kick_steps: [B] int64 device array; a
+ * step outside [0, n-1) means no kick for that walk.  Since ABI 2.
+ */
+int zmpc_rollout_kicks(const zmpc_plan* plan, int64_t B, int64_t n, const double* zmax,
+                       const double* zmin, int64_t bounds_stride, const double* x0,
+                       const double* kick, const int64_t* kick_steps, double* hist,
+                       int32_t* status, void* stream);
+
+/*
+ * Batched CoP-bound producer: CoPGenerator.generate_cop_trajectory
+ * (generators/cop_generator.py:34-115) over the footstep plan of
+ * generators/footstep_generator.py:19-49, one walk per set of parameters.
+ *   params : [B, 7] device doubles = distance, step_length, foot_spread, ssp_duration,
+ *            dsp_duration, standing_duration, dt (the reference's float clock t += dt is
+ *            reproduced exactly, so the sample counts match)
+ *   n_cap = 0: count only — n_out[b] = samples of walk b (int64 device array)
+ *   n_cap > 0: zmax, zmin [B, n_cap, 2] (rows past n_b repeat the walk's last row, the
+ *            rollout's own window padding), states [B, n_cap] int8 (0 STANDING,
+ *            1 DOUBLE_SUPPORT, 2 SINGLE_SUPPORT, -1 padding) or NULL, n_out or NULL.
+ * Since ABI 2.
+ */
+int zmpc_cop_generate(int device, int64_t B, const double* params, int64_t n_cap,
+                      double* zmax, double* zmin, int8_t* states, int64_t* n_out,
+                      void* stream);
 
 /* Message describing the last failure on the calling thread ("" if none). */
 const char* zmpc_last_error(void);

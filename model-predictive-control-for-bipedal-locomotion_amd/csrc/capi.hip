@@ -202,10 +202,10 @@ int zmpc_step(const zmpc_plan* P, int64_t B, const double* x, const double* zmax
   return ZMPC_OK;
 }
 
-int zmpc_rollout(const zmpc_plan* P, int64_t B, int64_t n, const double* zmax,
-                 const double* zmin, int64_t bounds_stride, const double* x0,
-                 const double* kick, int64_t kick_step, double* hist, int32_t* status,
-                 void* stream) {
+static int rollout_impl(const zmpc_plan* P, int64_t B, int64_t n, const double* zmax,
+                        const double* zmin, int64_t bounds_stride, const double* x0,
+                        const double* kick, int64_t kick_step, const int64_t* kick_steps,
+                        double* hist, int32_t* status, void* stream) {
   g_err.clear();
   if (!P) return fail(ZMPC_EINVAL, "NULL plan");
   if (B < 0 || n < 1) return fail(ZMPC_EINVAL, "need B >= 0 and n >= 1");
@@ -219,12 +219,55 @@ int zmpc_rollout(const zmpc_plan* P, int64_t B, int64_t n, const double* zmax,
   if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
   std::string why;
   hipStream_t s = (hipStream_t)stream;
-  hipError_t e = P->strict ? zmpc_launch_rollout_strict(P, B, n, zmax, zmin, bounds_stride, x0, kick, kick_step,
-                                                        hist, status, s, &why)
-                           : zmpc_launch_rollout_unc(P, B, n, zmax, zmin, bounds_stride, x0, kick, kick_step,
-                                                     hist, status, s, &why);
+  hipError_t e = P->strict ? zmpc_launch_rollout_strict(P, B, n, zmax, zmin, bounds_stride, x0,
+                                                        kick, kick_step, kick_steps, hist,
+                                                        status, s, &why)
+                           : zmpc_launch_rollout_unc(P, B, n, zmax, zmin, bounds_stride, x0,
+                                                     kick, kick_step, kick_steps, hist, status,
+                                                     s, &why);
   if (e != hipSuccess)
     return why.empty() ? hip_fail(e, "zmpc_rollout launch") : fail(ZMPC_EINVAL, why);
+  return ZMPC_OK;
+}
+
+int zmpc_rollout(const zmpc_plan* P, int64_t B, int64_t n, const double* zmax,
+                 const double* zmin, int64_t bounds_stride, const double* x0,
+                 const double* kick, int64_t kick_step, double* hist, int32_t* status,
+                 void* stream) {
+  return rollout_impl(P, B, n, zmax, zmin, bounds_stride, x0, kick, kick_step, nullptr, hist,
+                      status, stream);
+}
+
+int zmpc_rollout_kicks(const zmpc_plan* P, int64_t B, int64_t n, const double* zmax,
+                       const double* zmin, int64_t bounds_stride, const double* x0,
+                       const double* kick, const int64_t* kick_steps, double* hist,
+                       int32_t* status, void* stream) {
+  if (!kick_steps) {
+    g_err.clear();
+    return fail(ZMPC_EINVAL, "kick_steps is NULL (use zmpc_rollout for one kick step)");
+  }
+  return rollout_impl(P, B, n, zmax, zmin, bounds_stride, x0, kick, -1, kick_steps, hist,
+                      status, stream);
+}
+
+int zmpc_cop_generate(int device, int64_t B, const double* params, int64_t n_cap,
+                      double* zmax, double* zmin, int8_t* states, int64_t* n_out,
+                      void* stream) {
+  g_err.clear();
+  if (B < 0 || n_cap < 0) return fail(ZMPC_EINVAL, "need B >= 0 and n_cap >= 0");
+  if (B == 0) return ZMPC_OK;
+  if (!params) return fail(ZMPC_EINVAL, "params is NULL");
+  if (n_cap > 0 && (!zmax || !zmin)) return fail(ZMPC_EINVAL, "NULL output bounds");
+  if (n_cap == 0 && !n_out) return fail(ZMPC_EINVAL, "n_cap = 0 needs n_out");
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess) return hip_fail(e, "hipGetDeviceCount");
+  if (device < 0 || device >= ndev) return fail(ZMPC_EINVAL, "device index out of range");
+  DeviceGuard g(device);
+  if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
+  e = zmpc_launch_cop(B, params, n_cap, n_cap > 0 ? zmax : nullptr, n_cap > 0 ? zmin : nullptr,
+                      n_cap > 0 ? states : nullptr, n_out, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(e, "zmpc_cop_generate launch");
   return ZMPC_OK;
 }
 

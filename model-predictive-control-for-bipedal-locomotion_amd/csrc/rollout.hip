@@ -127,7 +127,13 @@ struct RolloutArgs {
   const double* scanP;  // [8][kScanLevels][9]: (Ā^C)^(2^r) for C = 1..8 (plan), or null
   int dbg;
   int srows;  // history rows the split-axis kernels stage per copy-out round
+  const int64_t* kick_steps;  // [B] per-walk kick steps (ragged walks), or null: kick_step
 };
+
+// The kick step of walk b: per walk (ragged batches) or the launch-wide one.
+__device__ __forceinline__ int64_t kick_step_of(const RolloutArgs& a, int64_t b) {
+  return a.kick_steps != nullptr ? a.kick_steps[b] : a.kick_step;
+}
 
 
 // Bounds of one walk held in registers: PF rounds of 64 samples, one 16-B (x, y) pair of
@@ -249,7 +255,7 @@ __device__ __forceinline__ void scan_replay_store(const RolloutArgs& a, int64_t 
   }
   const int C = REGF ? CW : (nsteps + 63) / 64;  // steps per lane chunk
   const int mbeg = lane * C;
-  const int64_t kick_step = a.kick_step;
+  const int64_t kick_step = kick_step_of(a, b);
 
   // ---- 3. affine scan of x_{i+1} = Ā x_i + B f_i (+ kick) over 64 lane chunks ----------
   double s0[3] = {0.0, 0.0, 0.0}, s1[3] = {0.0, 0.0, 0.0};
@@ -515,7 +521,7 @@ __device__ __forceinline__ void axis_finish(const RolloutArgs& a, int64_t b, int
   const double* xb = a.x0 + b * 6 + 3 * axis;
   const double xi[3] = {xb[0], xb[1], xb[2]};
   const double kk = (axis == 1 && a.kick != nullptr) ? a.kick[b] : 0.0;
-  const int64_t kick_step = (axis == 1) ? a.kick_step : -1;
+  const int64_t kick_step = (axis == 1) ? kick_step_of(a, b) : -1;
   const LipmConsts lc = a.lc;
   const double kx0 = a.kx[0], kx1 = a.kx[1], kx2 = a.kx[2];
   const double Bv[3] = {lc.T3_6, lc.T2_2, lc.T};
@@ -696,7 +702,7 @@ __device__ __forceinline__ void split_walk(const RolloutArgs& a, int64_t b, doub
   axis_correlate<CW>(a, kg, axis ? zr1 : zr0, lane, f);  // k: wave-uniform scalar loads
   __syncthreads();  // z_ref dead: the area becomes the history staging (n rows of 6)
   // ---- 4. lane-chunk affine scan -----------------------------------------------------------
-  const int64_t kick_step = (axis == 1) ? a.kick_step : -1;
+  const int64_t kick_step = (axis == 1) ? kick_step_of(a, b) : -1;
   const LipmConsts lc = a.lc;
   const double kx0 = kxp[0], kx1 = kxp[1], kx2 = kxp[2];
   const double Bv[3] = {lc.T3_6, lc.T2_2, lc.T};
@@ -864,7 +870,7 @@ __global__ void __launch_bounds__(128 * W, 4) zmpc_rollout_unc_wide_kernel(Rollo
   double f[CW];
   axis_correlate<CW>(a, a.k, (axis ? zr1 : zr0) + ZL::idx(w * 64 * CW), lane, f);
   // ---- 3. scan: per-wave zero-start Kogge-Stone, then the cross-wave offsets ---------------
-  const int64_t kick_step = (axis == 1) ? a.kick_step : -1;
+  const int64_t kick_step = (axis == 1) ? kick_step_of(a, b) : -1;
   const LipmConsts lc = a.lc;
   const double kx0 = a.kx[0], kx1 = a.kx[1], kx2 = a.kx[2];
   const double Bv[3] = {lc.T3_6, lc.T2_2, lc.T};
@@ -1169,8 +1175,9 @@ size_t zmpc_rollout_unc_lds_bytes(int N, int64_t n) { return lds_bytes(rollout_g
 
 hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, const double* zmax,
                                    const double* zmin, int64_t bstride, const double* x0,
-                                   const double* kick, int64_t kick_step, double* hist,
-                                   int32_t* status, hipStream_t s, std::string* why) {
+                                   const double* kick, int64_t kick_step,
+                                   const int64_t* kick_steps, double* hist, int32_t* status,
+                                   hipStream_t s, std::string* why) {
   if (n == 1) {
     // no QP solve: the history is the initial state only
     hipError_t e = hipMemcpyAsync(hist, x0, 6 * sizeof(double) * (size_t)B,
@@ -1191,7 +1198,7 @@ hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, con
   }();
   RolloutArgs a{g.kc, g.kcp, g.lz,      g.lzp, (int)n,     B,   p->lc,
                 p->k, p->kx,  zmax,      zmin,  bstride,    x0,  kick,
-                kick_step,    hist, status, p->scanP, dbg, 0};
+                kick_step,    hist, status, p->scanP, dbg, 0, kick_steps};
   WideGeom wg;
   static const bool no_wide = getenv("ZMPC_ROLLOUT_NO_WIDE") != nullptr;  // A/B: long kernel
   if (!no_wide && g.passes > 1 && wide_geom(p->N, n, &wg)) {

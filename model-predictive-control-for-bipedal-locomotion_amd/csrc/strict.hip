@@ -52,6 +52,7 @@ struct StrictArgs {
   const double* x0;      // rollout [B,2,3], step [B,3]
   const double* kick;    // [B] or null
   int64_t kick_step;
+  const int64_t* kick_steps;  // [B] per-walk kick steps, or null
   double* out;           // rollout hist [B,n,2,3], step x_next [B,3]
   int32_t* status;       // [B] or null
   double* scratch;       // per-wave N*N factor scratch (gridDim*SWAVES slots)
@@ -759,7 +760,8 @@ __global__ void __launch_bounds__(256) zmpc_strict_kernel(StrictArgs a) {
         const double u0 = solve_instance<NJ>(a, inst, i, xv, Wt + s * ld, st, w, lane, &fq);
         double xn[3];
         lipm_step(a.lc, xv, u0, xn);
-        if (!a.window_mode && (inst & 1) && i == a.kick_step && a.kick != nullptr)
+        if (!a.window_mode && (inst & 1) && a.kick != nullptr &&
+            i == (a.kick_steps ? a.kick_steps[inst >> 1] : a.kick_step))
           xn[1] -= a.kick[inst >> 1];
         if (!(isfinite(xn[0]) && isfinite(xn[1]) && isfinite(xn[2]))) fq |= ZMPC_ST_NONFINITE;
         if (lane == 0) fl[s] |= fq;
@@ -895,8 +897,8 @@ static hipError_t launch_strict(const zmpc_plan* p, StrictArgs a, hipStream_t s,
 hipError_t zmpc_launch_rollout_strict(const zmpc_plan* p, int64_t B, int64_t n,
                                       const double* zmax, const double* zmin, int64_t bstride,
                                       const double* x0, const double* kick, int64_t kick_step,
-                                      double* hist, int32_t* status, hipStream_t s,
-                                      std::string* why) {
+                                      const int64_t* kick_steps, double* hist, int32_t* status,
+                                      hipStream_t s, std::string* why) {
   if (!p->G) {
     *why = "plan was created without strict workspace";
     return hipErrorInvalidValue;
@@ -922,6 +924,7 @@ hipError_t zmpc_launch_rollout_strict(const zmpc_plan* p, int64_t B, int64_t n,
   a.x0 = x0;
   a.kick = kick;
   a.kick_step = kick_step;
+  a.kick_steps = kick_steps;
   a.out = hist;
   a.status = status;
   return launch_strict(p, a, s, why);

@@ -49,11 +49,16 @@ struct zmpc_plan {
 // kernels launchers (plan.hip)
 hipError_t zmpc_launch_plan(zmpc_plan* p, hipStream_t s);
 
+// batched CoP-bound producer (cop.hip): params [B][7] = distance, step_length, foot_spread,
+// ssp, dsp, standing, dt; n_cap = 0 counts only (n_out)
+hipError_t zmpc_launch_cop(int64_t B, const double* params, int64_t n_cap, double* zmax,
+                           double* zmin, int8_t* states, int64_t* n_out, hipStream_t s);
+
 // unconstrained rollout / step (rollout.hip)
 hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, const double* zmax,
                                    const double* zmin, int64_t bstride, const double* x0,
-                                   const double* kick,
-                                   int64_t kick_step, double* hist, int32_t* status,
+                                   const double* kick, int64_t kick_step,
+                                   const int64_t* kick_steps, double* hist, int32_t* status,
                                    hipStream_t s, std::string* why);
 hipError_t zmpc_launch_step_unc(const zmpc_plan* p, int64_t B, const double* x,
                                 const double* zmax_win, const double* zmin_win, double* x_next,
@@ -63,7 +68,8 @@ hipError_t zmpc_launch_step_unc(const zmpc_plan* p, int64_t B, const double* x,
 hipError_t zmpc_launch_rollout_strict(const zmpc_plan* p, int64_t B, int64_t n,
                                       const double* zmax, const double* zmin, int64_t bstride,
                                       const double* x0,
-                                      const double* kick, int64_t kick_step, double* hist,
+                                      const double* kick, int64_t kick_step,
+                                      const int64_t* kick_steps, double* hist,
                                       int32_t* status, hipStream_t s, std::string* why);
 hipError_t zmpc_launch_step_strict(const zmpc_plan* p, int64_t B, const double* x,
                                    const double* zmax_win, const double* zmin_win,

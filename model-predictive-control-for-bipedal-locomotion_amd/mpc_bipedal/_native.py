@@ -12,6 +12,8 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ZMPC_LIB", os.path.join(_HERE, "libzmpc.so"))
 
+ABI_VERSION = 2  # include/zmpc.h ZMPC_ABI_VERSION this binding is written for
+
 ZMPC_OK = 0
 ZMPC_EINVAL = -1
 ZMPC_EHIP = -2
@@ -42,6 +44,13 @@ SIGNATURES = {
     "zmpc_rollout": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, _c_dbl_p,
                                     _c_dbl_p, ctypes.c_int64, _c_dbl_p, _c_dbl_p, ctypes.c_int64,
                                     _c_dbl_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "zmpc_rollout_kicks": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                          _c_dbl_p, _c_dbl_p, ctypes.c_int64, _c_dbl_p, _c_dbl_p,
+                                          ctypes.c_void_p, _c_dbl_p, ctypes.c_void_p,
+                                          ctypes.c_void_p]),
+    "zmpc_cop_generate": (ctypes.c_int, [ctypes.c_int, ctypes.c_int64, _c_dbl_p, ctypes.c_int64,
+                                         _c_dbl_p, _c_dbl_p, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_void_p]),
 }
 
 _lib = None

@@ -119,7 +119,7 @@ class ZMPController:
 
     # ------------------------------------------------------------------ batched additions
     def generate_state_trajectory_batch(self, x_init, z_max, z_min, F_ext=None,
-                                        force_step: Optional[int] = None):
+                                        force_step: Optional[int] = None, walk_lengths=None):
         """Many walks at once; every input may be NumPy or a torch tensor.
 
         x_init : [B,2,3] initial (x-axis, y-axis) states, or None for zeros
@@ -127,6 +127,9 @@ class ZMPController:
         F_ext : None (no disturbance) or [B] forces in N; the y velocity at history index
                 force_step+1 drops by dt·F_ext/m (default force_step = n//2, as
                 zmp_controller.py:90,105-106)
+        walk_lengths : [B] sample counts of ragged walks padded to n with their last row
+                (CoPGenerator.generate_cop_batch); the force then hits step n_b//2 of each
+                walk and hist[b, :n_b] is walk b's history
         Returns (hist [B,n,2,3], status [B]) on the plan's device.
         """
         plan = self._plan()
@@ -143,16 +146,20 @@ class ZMPController:
         if F_ext is not None:
             F = torch.as_tensor(F_ext, dtype=torch.float64, device=dev).reshape(B)
             kick = self.config.dt * F / self.config.m
-        step = (n // 2) if force_step is None else int(force_step)
+        if walk_lengths is not None:
+            step = torch.as_tensor(walk_lengths, dtype=torch.int64, device=dev).reshape(B) // 2
+        else:
+            step = (n // 2) if force_step is None else int(force_step)
         hist, st = plan.rollout(zmax_t, z_min, x0, kick=kick, kick_step=step)
         if plan.strict:
             self._raise_on_status(st)
         return hist, st
 
     def generate_com_trajectory_batch(self, x_init, z_max, z_min, F_ext=None,
-                                      force_step: Optional[int] = None):
+                                      force_step: Optional[int] = None, walk_lengths=None):
         """Batched generate_com_trajectory_wieber: (com [B,n,2], hist [B,n,2,3]) on device."""
-        hist, _ = self.generate_state_trajectory_batch(x_init, z_max, z_min, F_ext, force_step)
+        hist, _ = self.generate_state_trajectory_batch(x_init, z_max, z_min, F_ext, force_step,
+                                                       walk_lengths)
         return hist[..., 0], hist
 
     def zmp(self, hist):

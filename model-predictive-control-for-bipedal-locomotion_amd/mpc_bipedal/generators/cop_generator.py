@@ -81,3 +81,49 @@ class CoPGenerator:
                 states.append(state)
             t += self.dt
         return np.array(upper), np.array(lower), states
+
+
+def cop_params(config) -> List[float]:
+    """The 7 producer parameters of a config, in zmpc_cop_generate's order."""
+    return [float(config.distance), float(config.step_length), float(config.foot_spread),
+            float(config.ssp_duration), float(config.dsp_duration),
+            float(config.standing_duration), float(config.dt)]
+
+
+def generate_cop_batch(params, device: int = 0):
+    """Batched device CoP producer (C-ABI zmpc_cop_generate).
+
+    params: a sequence of MPCConfig-like objects, or a [B, 7] array of (distance,
+    step_length, foot_spread, ssp_duration, dsp_duration, standing_duration, dt).
+    Returns device tensors (z_max [B, n_max, 2], z_min, n [B] int64, states [B, n_max] int8):
+    walk b is rows [0, n_b), rows past n_b repeat its last row (the rollout's own window
+    padding, so the padded batch rolls out each walk exactly); states use 0 STANDING,
+    1 DOUBLE_SUPPORT, 2 SINGLE_SUPPORT, -1 padding.  Bit-exact with generate_cop_trajectory.
+    """
+    import ctypes
+    import torch
+    from .. import _native
+
+    if not isinstance(params, (np.ndarray,)) and not hasattr(params, "shape"):
+        params = [cop_params(c) for c in params]
+    dev = torch.device("cuda", int(device))
+    p = torch.as_tensor(np.asarray(params, dtype=np.float64), device=dev).contiguous()
+    if p.dim() != 2 or p.shape[1] != 7:
+        raise ValueError(f"params must be [B, 7], got {tuple(p.shape)}")
+    B = int(p.shape[0])
+    lib = _native.load()
+    n = torch.zeros(B, dtype=torch.int64, device=dev)
+    with torch.cuda.device(dev):
+        stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+        rc = lib.zmpc_cop_generate(int(device), B, p.data_ptr(), 0, None, None, None,
+                                   n.data_ptr(), stream)
+        _native.check(rc, "zmpc_cop_generate")
+        n_cap = int(n.max().item()) if B else 0
+        zmax = torch.empty((B, n_cap, 2), dtype=torch.float64, device=dev)
+        zmin = torch.empty_like(zmax)
+        states = torch.empty((B, n_cap), dtype=torch.int8, device=dev)
+        if B and n_cap:
+            rc = lib.zmpc_cop_generate(int(device), B, p.data_ptr(), n_cap, zmax.data_ptr(),
+                                       zmin.data_ptr(), states.data_ptr(), None, stream)
+            _native.check(rc, "zmpc_cop_generate")
+    return zmax, zmin, n, states

@@ -104,34 +104,35 @@ class Plan:
         """Validate once and return a zero-argument callable that re-issues the same rollout
         launch on the current stream (one ctypes call, no tensor checks): for timing loops
         and graph capture.  The tensors must stay alive while the launcher is used."""
-        hist, status, (args, keep) = self._rollout_args(zmax, zmin, x0, kick, kick_step, hist,
-                                                        status)
-        fn = _native.load().zmpc_rollout
+        hist, status, (name, args, keep) = self._rollout_args(zmax, zmin, x0, kick, kick_step,
+                                                              hist, status)
+        fn = getattr(_native.load(), name)
         dev = self.device
 
         def launch():
             stream = torch.cuda.current_stream(dev).cuda_stream
             rc = fn(*args, ctypes.c_void_p(stream))
             if rc != 0:
-                _native.check(rc, "zmpc_rollout")
+                _native.check(rc, name)
         launch.hist, launch.status, launch.inputs = hist, status, keep
         return launch
 
     def rollout(self, zmax, zmin, x0, kick=None, kick_step=-1, hist=None, status=None):
         """Batched Wieber rollout → hist [B,n,2,3] (device), status [B] (see _rollout_args)."""
-        hist, status, (args, _) = self._rollout_args(zmax, zmin, x0, kick, kick_step, hist,
-                                                     status)
+        hist, status, (name, args, _) = self._rollout_args(zmax, zmin, x0, kick, kick_step, hist,
+                                                           status)
         with torch.cuda.device(self.device):
             stream = torch.cuda.current_stream(self.device).cuda_stream
-            rc = _native.load().zmpc_rollout(*args, ctypes.c_void_p(stream))
-        _native.check(rc, "zmpc_rollout")
+            rc = getattr(_native.load(), name)(*args, ctypes.c_void_p(stream))
+        _native.check(rc, name)
         return hist, status
 
     def _rollout_args(self, zmax, zmin, x0, kick, kick_step, hist, status):
         """Batched Wieber rollout → hist [B,n,2,3] (device), status [B].
 
         zmax/zmin: [B,n,2] per-walk CoP bounds, or [n,2] one CoP shared by every walk;
-        x0: [B,2,3]; kick: [B] velocity impulse subtracted from y at step kick_step.
+        x0: [B,2,3]; kick: [B] velocity impulse subtracted from y at step kick_step — an int,
+        or a [B] array of per-walk steps (ragged walks: zmpc_rollout_kicks).
         """
         zmax = self._as_dev(zmax)
         x0 = self._as_dev(x0)
@@ -157,9 +158,16 @@ class Plan:
                              "plan's device")
         if status is None:
             status = torch.empty(B, dtype=torch.int32, device=self._dev())
+        if isinstance(kick_step, (int, np.integer)):
+            args = (self._h, B, n, _ptr(zmax), _ptr(zmin), bstride, _ptr(x0), _ptr(kick_t),
+                    int(kick_step), _ptr(hist), _ptr(status))
+            return hist, status, ("zmpc_rollout", args, (zmax, zmin, x0, kick_t))
+        ks = torch.as_tensor(kick_step, dtype=torch.int64, device=self._dev()).contiguous()
+        if tuple(ks.shape) != (B,):
+            raise ValueError(f"per-walk kick_step must be [B], got {tuple(ks.shape)}")
         args = (self._h, B, n, _ptr(zmax), _ptr(zmin), bstride, _ptr(x0), _ptr(kick_t),
-                int(kick_step), _ptr(hist), _ptr(status))
-        return hist, status, (args, (zmax, zmin, x0, kick_t))
+                _ptr(ks), _ptr(hist), _ptr(status))
+        return hist, status, ("zmpc_rollout_kicks", args, (zmax, zmin, x0, kick_t, ks))
 
 
 def get_plan(config, device=None) -> Plan:

@@ -163,6 +163,74 @@ def test_cli_matches_reference_walk(tmp_path):
     assert rmse(r3["com"][1], d["com_force"]) <= 1e-9
 
 
+def _cop_cases():
+    """The 7 golden CoP configurations + seeded random walk parameters (ragged n)."""
+    from mpc_bipedal.generators import cop_params
+    cases = []
+    for tag in ("default_n150", "default_n10", "default_n64", "default_n512",
+                "classdefaults_n150", "long_n100", "short_n200"):
+        d = golden(f"cop_{tag}.npz")
+        cases.append(MPCConfig(horizon=int(d["horizon"]), dt=float(d["dt"]),
+                               distance=float(d["distance"]),
+                               step_length=float(d["step_length"]),
+                               foot_spread=float(d["foot_spread"]),
+                               ssp_duration=float(d["ssp_duration"]),
+                               dsp_duration=float(d["dsp_duration"]),
+                               standing_duration=float(d["standing_duration"])))
+    rng = np.random.default_rng(8)
+    for _ in range(25):
+        cases.append(MPCConfig(horizon=150, distance=float(rng.uniform(0.2, 4.0)),
+                               step_length=float(rng.uniform(0.1, 0.45)),
+                               foot_spread=float(rng.uniform(0.05, 0.15)),
+                               ssp_duration=float(rng.uniform(0.1, 0.5)),
+                               dsp_duration=float(rng.uniform(0.01, 0.1)),
+                               standing_duration=float(rng.uniform(0.2, 1.5))))
+    return cases, np.array([cop_params(c) for c in cases])
+
+
+def test_device_cop_producer_bit_exact():
+    """zmpc_cop_generate vs the host generator (itself bit-exact vs the
+    reference fixtures): every walk's bounds, states and sample count, padding rows."""
+    from mpc_bipedal.generators import CoPGenerator, State, generate_cop_batch
+    cases, params = _cop_cases()
+    zx, zn, n, st = generate_cop_batch(params)
+    zx, zn, n, st = zx.cpu().numpy(), zn.cpu().numpy(), n.cpu().numpy(), st.cpu().numpy()
+    code = {State.STANDING: 0, State.DOUBLE_SUPPORT: 1, State.SINGLE_SUPPORT: 2}
+    for b, c in enumerate(cases):
+        hx, hn, hs = CoPGenerator(c).generate_cop_trajectory()
+        nb = len(hx)
+        assert n[b] == nb, b
+        assert np.array_equal(zx[b, :nb], hx) and np.array_equal(zn[b, :nb], hn), b
+        assert np.array_equal(st[b, :nb], [code[s] for s in hs]), b
+        assert (zx[b, nb:] == hx[-1]).all() and (zn[b, nb:] == hn[-1]).all()
+        assert (st[b, nb:] == -1).all()
+
+
+def test_ragged_batch_rollout_equals_single_walks():
+    """Ragged walks from the device producer, padded to the longest, in ONE rollout with a
+    per-walk force step (n_b // 2, zmp_controller.py:90) == each walk run alone through the
+    drop-in API (generate_com_trajectory_wieber)."""
+    from mpc_bipedal.generators import CoPGenerator, generate_cop_batch
+    cases, params = _cop_cases()
+    cases = [c for c in cases if abs(c.dt - 0.01) < 1e-15][:12]
+    params = params[[i for i, c in enumerate(_cop_cases()[0]) if abs(c.dt - 0.01) < 1e-15][:12]]
+    zx, zn, n, _ = generate_cop_batch(params)
+    B = len(cases)
+    F = np.linspace(100.0, 800.0, B)
+    cfg = MPCConfig(horizon=150, strict=False, add_force=True)
+    ctl = ZMPController(cfg)
+    com, hist = ctl.generate_com_trajectory_batch(np.zeros((B, 2, 3)), zx, zn, F_ext=F,
+                                                  walk_lengths=n)
+    com = com.cpu().numpy()
+    for b, c in enumerate(cases):
+        hx, hn, _ = CoPGenerator(c).generate_cop_trajectory()
+        one = ZMPController(MPCConfig(horizon=150, strict=False, add_force=True,
+                                      F_ext=float(F[b])))
+        ref, _ = one.generate_com_trajectory_wieber(np.zeros((3, 1)), np.zeros((3, 1)), hx, hn)
+        nb = int(n[b])
+        assert np.abs(com[b, :nb] - ref).max() <= 1e-12, b
+
+
 # --------------------------------------------------------------------------- batches
 
 

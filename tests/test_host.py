@@ -92,7 +92,7 @@ def test_library_loads_and_exports_every_symbol():
     exported = set(re.findall(r" T (zmpc_\w+)", out))
     assert set(_header_symbols()) <= exported
     lib = _native.load()
-    assert lib.zmpc_abi_version() == 1
+    assert lib.zmpc_abi_version() == _native.ABI_VERSION == 2
     assert lib.zmpc_last_error() == b""
 
 
@@ -109,6 +109,12 @@ def test_argument_errors_without_gpu():
     assert rc == _native.ZMPC_EINVAL
     rc = lib.zmpc_step(None, 1, None, None, None, None, None, None)
     assert rc == _native.ZMPC_EINVAL
+    rc = lib.zmpc_rollout_kicks(None, 1, 10, None, None, 20, None, None, None, None, None, None)
+    assert rc == _native.ZMPC_EINVAL and b"kick_steps" in lib.zmpc_last_error()
+    rc = lib.zmpc_cop_generate(0, -1, None, 0, None, None, None, None, None)
+    assert rc == _native.ZMPC_EINVAL
+    rc = lib.zmpc_cop_generate(0, 4, None, 0, None, None, None, None, None)
+    assert rc == _native.ZMPC_EINVAL and b"params" in lib.zmpc_last_error()
 
 
 def test_router_errors():
