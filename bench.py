@@ -190,6 +190,10 @@ def main():
     ap.add_argument("--unconstrained", action="store_true", help="config 4 unconstrained variant")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pipelined", action="store_true",
+                    help="also time batches pipelined two-deep on two streams (reported beside "
+                         "value; off by default so a profile of the default command sees only "
+                         "non-overlapped launches)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -290,7 +294,7 @@ def main():
     # rollouts overlap, so one's memory phases run under the other's FP64 phases — what a
     # many-batch driver gets; reported beside `value`, not as it
     pipelined = None
-    if rank == 0 and world == 1 and not cfg.strict:
+    if rank == 0 and world == 1 and not cfg.strict and args.pipelined:
         streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
         hist2 = torch.empty_like(hist)
         with torch.cuda.stream(streams[1]):
