@@ -71,6 +71,14 @@ int zmpc_plan_create(int device, int32_t N, double T, double T2_2, double T3_6, 
   if (device < 64 && !attrs_done[device]) {
     if ((e = zmpc_rollout_unc_set_attrs()) != hipSuccess) return hip_fail(e, "set LDS attrs");
     if ((e = zmpc_strict_set_attrs()) != hipSuccess) return hip_fail(e, "set LDS attrs");
+    if ((e = zmpc_strict_lq_set_attrs()) != hipSuccess) return hip_fail(e, "set LDS attrs");
+    // the strict solver's per-launch workspace comes from the stream-ordered pool: keep
+    // freed blocks in the pool instead of returning them to the driver at every sync
+    hipMemPool_t pool = nullptr;
+    if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess && pool) {
+      uint64_t keep = ~0ull;
+      (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+    }
     attrs_done[device] = true;
   }
 

@@ -894,11 +894,22 @@ static hipError_t launch_strict(const zmpc_plan* p, StrictArgs a, hipStream_t s,
   return e;
 }
 
+// ZMPC_STRICT_VARIANT=chol selects this file's reduced-Cholesky kernel (A/B and cross-checks);
+// the default is the LQ-form kernel of strict_lq.hip.
+static bool use_chol_variant(const zmpc_plan* p) {
+  static const char* v = getenv("ZMPC_STRICT_VARIANT");
+  static const bool chol = v != nullptr && std::string(v) == "chol";
+  return chol || !zmpc_strict_lq_supported(p);
+}
+
 hipError_t zmpc_launch_rollout_strict(const zmpc_plan* p, int64_t B, int64_t n,
                                       const double* zmax, const double* zmin, int64_t bstride,
                                       const double* x0, const double* kick, int64_t kick_step,
                                       const int64_t* kick_steps, double* hist, int32_t* status,
                                       hipStream_t s, std::string* why) {
+  if (!use_chol_variant(p) && n > 1)
+    return zmpc_launch_rollout_strict_lq(p, B, n, zmax, zmin, bstride, x0, kick, kick_step,
+                                         kick_steps, hist, status, s, why);
   if (!p->G) {
     *why = "plan was created without strict workspace";
     return hipErrorInvalidValue;
@@ -934,6 +945,8 @@ hipError_t zmpc_launch_step_strict(const zmpc_plan* p, int64_t B, const double* 
                                    const double* zmax_win, const double* zmin_win,
                                    double* x_next, int32_t* status, hipStream_t s,
                                    std::string* why) {
+  if (!use_chol_variant(p))
+    return zmpc_launch_step_strict_lq(p, B, x, zmax_win, zmin_win, x_next, status, s, why);
   if (!p->G) {
     *why = "plan was created without strict workspace";
     return hipErrorInvalidValue;

@@ -1,0 +1,671 @@
+// Strict (ZMP box-constrained) Wieber QP, one instance per lane, solved in LQ form.
+//
+// Reference, per axis and timestep (zmp_controller.py:173-195, cvxpy→OSQP there):
+//   min_J ½Q‖Px x + Pu J − z_ref‖² + ½R‖J‖²   s.t.  z_min ≤ Px x + Pu J ≤ z_max,  u0 = J[0]
+// Pu[k,j] = C A^(k−j) B and Px[k] = C A^(k+1) (zmp_controller.py:162-171), so the predicted ZMP
+// is the output of the LIPM itself: with x_0 = x and x_{k+1} = A x_k + B u_k,
+//   z_k = C x_{k+1} = c1ᵀ x_k + p0 u_k,     c1 = (CA)ᵀ = [1, T, T²/2 − h/g],  p0 = CB = p(0).
+// The QP is a linear-quadratic tracking problem over the horizon with one output bound per
+// step.  For a working set (slot k active at t_k = z_max or z_min) the equality-constrained
+// problem is solved exactly by a backward Riccati recursion: a free step minimises over u_k,
+// an active step has u_k = (t_k − c1ᵀx_k)/p0 forced (p0 ≠ 0).  One unified update covers both
+// (u = −K x − kff; K = Qux/Quu or c1/p0):
+//   P ← Qxx − Qux_i K_j + K_i D_j,   s ← −qx + K qu − kff D,   D = Quu K − Qux (0 when free)
+// with Qxx = Q c1c1ᵀ + AᵀPA, Qux = Q p0 c1 + BᵀPA, Quu = Q p0² + R + BᵀPB, qu = −Q p0 r − Bᵀs,
+// qx = −Q r c1 − Aᵀs for the value function V(x) = ½xᵀPx − sᵀx.  The forward pass rolls the
+// trajectory out and recovers, from λ_{k+1} = ∇V_{k+1}(x_{k+1}) = P x_{k+1} − s, the bound
+// multipliers ν_k = −(R u_k + Bᵀλ_{k+1})/p0 − Q (t_k − r_k) of the active slots (the same ν
+// as the z-space KKT  H δ − W + ν = 0 of strict.hip: ≥ 0 at upper, ≤ 0 at lower bounds).
+// The working set comes from the same primal-dual active-set iteration as strict.hip —
+// warm-started with the previous timestep's set shifted one slot, release wrong-signed
+// multipliers, add violated free slots, stop when the set repeats — so the iterates and the
+// solution are the same, at O(N) per pass instead of a reduced Cholesky.
+//
+// Mapping: a lane owns one instance (one walk, one axis) for the whole rollout; a wave holds
+// 64 walks of one axis, in time lockstep (a wave's passes per timestep = the max over its
+// lanes; converged lanes are masked off).  The bounds come in [axis][t][walk] (a staging
+// transpose), so a wave's load of one window slot is 512 contiguous bytes.  Per pass:
+//   sweep A  backward Riccati over the horizon in segments of S steps, checkpointing (P, s)
+//            at segment boundaries to a per-lane global slab (coalesced [.., 9, 64]);
+//   sweep B  per segment from the front: reload its checkpoint, recompute its S Riccati
+//            steps into registers (K, kff, PB, Bᵀs, bounds, flags), roll forward through it,
+//            check primal/dual feasibility, update the slot flags (LDS, [N][64] bytes).
+// Everything a pass touches besides the bounds and the checkpoints lives in registers.
+#include <cstdio>
+#include <cstdlib>
+
+#include "zmpc_internal.h"
+
+namespace {
+
+constexpr int LQ_WAVES = 4;      // independent waves per workgroup
+constexpr int LQ_MAXIT = 64;     // active-set pass cap (as strict.hip)
+
+struct LqArgs {
+  int N, NS;             // horizon, segments ⌈N/S⌉
+  int toff;              // window slot k reads time i + toff + k (1 rollout, 0 step)
+  int window_mode;
+  int64_t n;             // samples per walk (rollout; 1 in window mode)
+  int64_t nsteps;        // timesteps (n − 1, or 1)
+  int64_t B;             // walks (rollout) or instances (step)
+  // staged bounds, tiled [axis][group of 64 walks][row][64]: row t of a window slot holds the
+  // group's 64 values for time t (rows past n − 1 repeat the last sample — the window padding
+  // of zmp_controller.py:81-88 — so no clamping in the kernel)
+  int64_t rows;          // rows per (axis, group)
+  int64_t groups;        // groups per axis in the staging (1 for a shared CoP)
+  int shared;            // 1: every walk reads group 0 (bounds_stride = 0)
+  const double* zmax;
+  const double* zmin;
+  const double* x0;      // rollout [B,2,3], step [B,3]
+  const double* kick;    // [B] or null
+  int64_t kick_step;
+  const int64_t* kick_steps;
+  double* out;           // rollout hist [B,n,2,3], step x_next [B,3]
+  int32_t* status;
+  double* ck;            // checkpoints [waves][NS][9][64]
+  unsigned long long* dbg;  // ZMPC_DEBUG_STRICT counters, null normally
+  // LIPM / QP constants.  The passes run in scaled coordinates ξ = [x0, T x1, T² x2],
+  // v = T³ u, objective divided by Q: Â = [[1,1,½],[0,1,1],[0,0,1]], B̂ = [⅙, ½, 1],
+  // z = ĉᵀξ + π v with ĉ = [1, 1, γ], γ = ½ − (h/g)/T², π = ⅙ − (h/g)/T² (= p(0)/T³),
+  // cost ½(z − r)² + ½ρ v², ρ = R/(Q T⁶).  Few distinct constants, most of them inline.
+  double T, T2, T3;      // reference-form state advance (zmp_controller.py:18-20,199)
+  double Tsq, Tcu;       // T², T³ (coordinate scaling)
+  double gam, pi, ipi;   // γ, π, 1/π
+  double rho, quu0;      // ρ, π² + ρ
+  double gipi, gam2, pig;  // γ/π, γ², πγ
+  double tolnu;          // multiplier tolerance in the scaled objective (1e-13 / Q)
+};
+
+struct Ric {  // value function V(x) = ½xᵀPx − sᵀx
+  double p00, p01, p02, p11, p12, p22, s0, s1, s2;
+};
+
+template <int S>
+struct SegIn {  // a segment's window slots: bounds and working-set flags
+  double hi[S], lo[S];
+  int f[S];
+};
+
+template <int S>
+struct SegOut {  // a segment's feedback (u = −K x − kff) and forward outputs, per step
+  double K0[S], K1[S], K2[S], kf[S];
+  double w[S];  // forward: Q (z_k − r_k) at free slots, u_k at active slots
+};
+
+// One backward Riccati step in scaled coordinates (see header and LqArgs).  Inputs: V_{k+1}
+// in v, slot flag f, bounds.  Outputs the step's feedback v_k = −K ξ_k − kff.
+__device__ __forceinline__ void ric_step(const LqArgs& a, Ric& v, double hi, double lo, int f,
+                                         double& K0, double& K1, double& K2, double& kf) {
+  constexpr double h = 0.5, s6 = 1.0 / 6.0;
+  // P B̂, B̂ᵀs, B̂ᵀPB̂
+  const double pb0 = fma(s6, v.p00, fma(h, v.p01, v.p02));
+  const double pb1 = fma(s6, v.p01, fma(h, v.p11, v.p12));
+  const double pb2 = fma(s6, v.p02, fma(h, v.p12, v.p22));
+  const double sb = fma(s6, v.s0, fma(h, v.s1, v.s2));
+  const double bpb = fma(s6, pb0, fma(h, pb1, pb2));
+  // P Â (columns 1, 2) and ÂᵀPÂ
+  const double m01 = v.p00 + v.p01, m02 = fma(h, v.p00, v.p01 + v.p02);
+  const double m11 = v.p01 + v.p11, m12 = fma(h, v.p01, v.p11 + v.p12);
+  const double m22 = fma(h, v.p02, v.p12 + v.p22);
+  const double S11 = m01 + m11, S12 = m02 + m12, S22 = fma(h, m02, m12 + m22);
+  // Qux = π ĉ + (PB̂)ᵀÂ, Quu, qu, −qx = r ĉ + Âᵀs
+  const double ux0 = a.pi + pb0;
+  const double ux1 = a.pi + (pb0 + pb1);
+  const double ux2 = a.pig + fma(h, pb0, pb1 + pb2);
+  const double Quu = a.quu0 + bpb;
+  const double r = (hi + lo) / 2;  // z_ref (zmp_controller.py:184)
+  const double qu = -fma(a.pi, r, sb);
+  const double nqx0 = r + v.s0;
+  const double nqx1 = r + (v.s0 + v.s1);
+  const double nqx2 = fma(a.gam, r, fma(h, v.s0, v.s1 + v.s2));
+  const bool act = f != 0;
+  const double iq = 1.0 / Quu;
+  const double t = (f == 1) ? hi : lo;
+  K0 = act ? a.ipi : ux0 * iq;
+  K1 = act ? a.ipi : ux1 * iq;
+  K2 = act ? a.gipi : ux2 * iq;
+  kf = act ? -t * a.ipi : qu * iq;
+  const double D0 = act ? fma(Quu, K0, -ux0) : 0.0;
+  const double D1 = act ? fma(Quu, K1, -ux1) : 0.0;
+  const double D2 = act ? fma(Quu, K2, -ux2) : 0.0;
+  // P = ĉĉᵀ + ÂᵀPÂ − Qux Kᵀ + K Dᵀ   (ĉĉᵀ = [[1,1,γ],[1,1,γ],[γ,γ,γ²]])
+  const double P00 = fma(K0, D0, fma(-ux0, K0, 1.0 + v.p00));
+  const double P01 = fma(K0, D1, fma(-ux0, K1, 1.0 + m01));
+  const double P02 = fma(K0, D2, fma(-ux0, K2, a.gam + m02));
+  const double P11 = fma(K1, D1, fma(-ux1, K1, 1.0 + S11));
+  const double P12 = fma(K1, D2, fma(-ux1, K2, a.gam + S12));
+  const double P22 = fma(K2, D2, fma(-ux2, K2, a.gam2 + S22));
+  v.s0 = fma(-kf, D0, fma(K0, qu, nqx0));
+  v.s1 = fma(-kf, D1, fma(K1, qu, nqx1));
+  v.s2 = fma(-kf, D2, fma(K2, qu, nqx2));
+  v.p00 = P00;
+  v.p01 = P01;
+  v.p02 = P02;
+  v.p11 = P11;
+  v.p12 = P12;
+  v.p22 = P22;
+}
+
+struct Lane {
+  const double* hi;  // wave's staged z_max rows (uniform)
+  const double* lo;  // wave's staged z_min rows
+  int lane;
+};
+
+// Issue the loads of segment j's slots (bounds, flags).  Slots past N are clamped to N − 1
+// (loaded, never used) so the loads carry no guards and can be issued a segment ahead.
+template <int S>
+__device__ __forceinline__ void seg_load(const LqArgs& a, int j, const Lane& L, int64_t i,
+                                         const unsigned char* fl, SegIn<S>& in) {
+  // segment's first row (uniform); the S rows are 512 B apart: one base, immediate offsets
+  const int64_t row0 = i + a.toff + (int64_t)j * S;
+  const double* hp = L.hi + row0 * 64;
+  const double* lp = L.lo + row0 * 64;
+  const unsigned char* fp = fl + j * S * 64;
+#pragma unroll
+  for (int q = 0; q < S; ++q) {
+    in.hi[q] = hp[q * 64 + L.lane];
+    in.lo[q] = lp[q * 64 + L.lane];
+    in.f[q] = fp[q * 64 + L.lane];
+  }
+}
+
+// Riccati steps of segment j (slots jS + S−1 down to jS).  KEEP: feedback kept in g (sweep
+// B) or dropped (sweep A).  FULL: every slot of the segment is < N (straight-line code).
+template <int S, bool FULL, bool KEEP>
+__device__ __forceinline__ void seg_riccati(const LqArgs& a, int j, Ric& v, const SegIn<S>& in,
+                                            SegOut<S>& g) {
+#pragma unroll
+  for (int q = S - 1; q >= 0; --q) {
+    const int k = j * S + q;
+    if (FULL || k < a.N) {
+      double K0, K1, K2, kf;
+      ric_step(a, v, in.hi[q], in.lo[q], in.f[q], K0, K1, K2, kf);
+      if (KEEP) {
+        g.K0[q] = K0;
+        g.K1[q] = K1;
+        g.K2[q] = K2;
+        g.kf[q] = kf;
+      }
+    }
+    // keep each step's work inside the step: hoisting the load-dependent parts of all S
+    // steps ahead of the recursion buys nothing (the chain is serial) and costs registers
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+// Forward through segment j: roll the trajectory out (x advances to the segment's end),
+// primal check of the free slots, and the per-step input of the costate sweep.
+template <int S, bool FULL>
+__device__ __forceinline__ void seg_forward(const LqArgs& a, int j, const SegIn<S>& in, SegOut<S>& g,
+                                            double* x, double& u0, bool& changed,
+                                            unsigned char* fl, int lane) {
+  constexpr double h = 0.5, s6 = 1.0 / 6.0;
+  const double tol = 1e-13;  // as strict.hip (tolz)
+#pragma unroll
+  for (int q = 0; q < S; ++q) {
+    const int k = j * S + q;
+    if (FULL || k < a.N) {
+      const double u = -fma(g.K0[q], x[0], fma(g.K1[q], x[1], g.K2[q] * x[2])) - g.kf[q];
+      if (k == 0) u0 = u;
+      const double z = fma(a.pi, u, fma(a.gam, x[2], x[0] + x[1]));
+      const double y0 = fma(s6, u, fma(h, x[2], x[0] + x[1]));
+      const double y1 = fma(h, u, x[1] + x[2]);
+      const double y2 = x[2] + u;
+      x[0] = y0;
+      x[1] = y1;
+      x[2] = y2;
+      const int f = in.f[q];
+      const double hi = in.hi[q], lo = in.lo[q];
+      const double r = (hi + lo) / 2;
+      g.w[q] = (f == 0) ? z - r : u;
+      if (f == 0) {
+        const int nf = (z > hi + tol) ? 1 : ((z < lo - tol) ? 2 : 0);
+        if (nf != 0) {
+          fl[k * 64 + lane] = (unsigned char)nf;
+          changed = true;
+        }
+      }
+    }
+  }
+}
+
+// Costate sweep back through segment j from λ at its end (λ_k = ∇V_k(x_k) = c1 e_k + Aᵀλ_{k+1},
+// e_k = Q (z_k − r_k) + ν_k): the bound multipliers ν_k of the active slots, dual check.
+template <int S, bool FULL>
+__device__ __forceinline__ void seg_costate(const LqArgs& a, int j, const SegIn<S>& in,
+                                            const SegOut<S>& g, double* lam, bool& changed,
+                                            unsigned char* fl, int lane) {
+  constexpr double h = 0.5, s6 = 1.0 / 6.0;
+#pragma unroll
+  for (int q = S - 1; q >= 0; --q) {
+    const int k = j * S + q;
+    if (FULL || k < a.N) {
+      const int f = in.f[q];
+      const double hi = in.hi[q], lo = in.lo[q];
+      const double bl = fma(s6, lam[0], fma(h, lam[1], lam[2]));  // B̂ᵀλ_{k+1}
+      // active: π e + ρ v + B̂ᵀλ_{k+1} = 0 (stationarity in v_k)
+      const double e = (f == 0) ? g.w[q] : -fma(a.rho, g.w[q], bl) * a.ipi;
+      if (f != 0) {
+        const double r = (hi + lo) / 2;
+        const double t = (f == 1) ? hi : lo;
+        const double nu = e - (t - r);  // ν / Q
+        if ((f == 1 && nu < -a.tolnu) || (f == 2 && nu > a.tolnu)) {
+          fl[k * 64 + lane] = 0;
+          changed = true;
+        }
+      }
+      const double l0 = lam[0], l1 = lam[1], l2 = lam[2];
+      lam[0] = e + l0;
+      lam[1] = e + (l0 + l1);
+      lam[2] = fma(a.gam, e, fma(h, l0, l1 + l2));
+    }
+  }
+}
+
+__device__ __forceinline__ void ck_store(const LqArgs& a, double* ck, int j, const Ric& v,
+                                         int lane) {
+  double* p = ck + (size_t)j * 9 * 64;
+  p += lane;
+  p[0] = v.p00;
+  p[64] = v.p01;
+  p[128] = v.p02;
+  p[192] = v.p11;
+  p[256] = v.p12;
+  p[320] = v.p22;
+  p[384] = v.s0;
+  p[448] = v.s1;
+  p[512] = v.s2;
+}
+
+__device__ __forceinline__ void ck_load(const double* ck, int j, Ric& v, int lane) {
+  const double* p = ck + (size_t)j * 9 * 64 + lane;
+  v.p00 = p[0];
+  v.p01 = p[64];
+  v.p02 = p[128];
+  v.p11 = p[192];
+  v.p12 = p[256];
+  v.p22 = p[320];
+  v.s0 = p[384];
+  v.s1 = p[448];
+  v.s2 = p[512];
+}
+
+template <int S, int W>
+__global__ void __launch_bounds__(64 * LQ_WAVES, W) zmpc_strict_lq_kernel(LqArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lq_smem[];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int64_t gw = (int64_t)blockIdx.x * LQ_WAVES + wave;
+  const int N = a.N;
+  // slot flags [NS·S][64] (rows past N stay 0: the last segment's loads are unguarded)
+  unsigned char* fl = lq_smem + (size_t)wave * a.NS * S * 64;
+  double* ck = a.ck + (size_t)gw * a.NS * 9 * 64;
+  int axis;
+  int64_t b0;
+  if (a.window_mode) {
+    axis = 0;
+    b0 = gw * 64;
+  } else {
+    axis = (int)(gw & 1);
+    b0 = (gw >> 1) * 64;
+  }
+  const int64_t b = b0 + lane;
+  const bool valid = b < a.B;
+  Lane L;
+  L.lane = lane;
+  {
+    const int64_t g = a.shared ? 0 : (b0 >> 6);
+    const int64_t off = ((int64_t)axis * a.groups + g) * a.rows * 64;
+    L.hi = a.zmax + off;
+    L.lo = a.zmin + off;
+  }
+  const int jfull = N / S;  // segments [0, jfull) are full
+  for (int k = 0; k < a.NS * S; ++k) fl[k * 64 + lane] = 0;
+
+  double x[3] = {0.0, 0.0, 0.0};
+  if (valid) {
+    const double* xp = a.window_mode ? a.x0 + b * 3 : a.x0 + (b * 2 + axis) * 3;
+    x[0] = xp[0];
+    x[1] = xp[1];
+    x[2] = xp[2];
+    if (!a.window_mode) {
+      double* h = a.out + ((b * a.n) * 2 + axis) * 3;  // hist[b, 0, axis, :] = x0
+      h[0] = x[0];
+      h[1] = x[1];
+      h[2] = x[2];
+    }
+  }
+  int fq = 0;
+  unsigned long long n_wave_pass = 0, n_lane_pass = 0;
+  const int64_t kstep =
+      (!a.window_mode && axis == 1 && a.kick != nullptr && valid)
+          ? (a.kick_steps ? a.kick_steps[b] : a.kick_step)
+          : -1;
+  const double kv = (kstep >= 0) ? a.kick[b] : 0.0;
+
+  for (int64_t i = 0; i < a.nsteps; ++i) {
+    if (i > 0) {
+      // warm start: the previous set shifted one slot towards the present (slot N−1 kept)
+      const int bytes = (N - 1) * 64;
+      for (int c = 0; c < bytes; c += 1024) {
+        const int o = c + lane * 16;
+        if (o < bytes) {
+          const uint4 vv = *reinterpret_cast<const uint4*>(fl + o + 64);
+          *reinterpret_cast<uint4*>(fl + o) = vv;
+        }
+      }
+    }
+    bool conv = !valid;
+    int it = 0;
+    double u0 = 0.0;
+    while (__any(!conv)) {
+      ++n_wave_pass;
+      if (!conv) {
+        ++n_lane_pass;
+        Ric v{0, 0, 0, 0, 0, 0, 0, 0, 0};
+        SegIn<S> cur, nxt;
+        SegOut<S> g;
+        // sweep A: full backward Riccati, checkpoints at segment boundaries; the next
+        // segment's loads are in flight under the current segment's recursion
+        seg_load(a, a.NS - 1, L, i, fl, cur);
+#pragma unroll 1
+        for (int j = a.NS - 1; j >= 0; --j) {
+          if (j > 0) seg_load(a, j - 1, L, i, fl, nxt);
+          ck_store(a, ck, j, v, lane);
+          if (j < jfull)
+            seg_riccati<S, true, false>(a, j, v, cur, g);
+          else
+            seg_riccati<S, false, false>(a, j, v, cur, g);
+          cur = nxt;
+        }
+        // sweep B: per segment from the front — recompute its Riccati steps from the
+        // checkpoint, forward, then the costate back through it from λ at its end
+        double xs[3] = {x[0], a.T * x[1], a.Tsq * x[2]};  // ξ
+        bool changed = false;
+        seg_load(a, 0, L, i, fl, cur);
+        Ric vn;
+        ck_load(ck, 0, v, lane);
+#pragma unroll 1
+        for (int j = 0; j < a.NS; ++j) {
+          if (j + 1 < a.NS) {
+            seg_load(a, j + 1, L, i, fl, nxt);
+            ck_load(ck, j + 1, vn, lane);
+          }
+          const Ric ve = v;  // V at the segment's end
+          if (j < jfull)
+            seg_riccati<S, true, true>(a, j, v, cur, g);
+          else
+            seg_riccati<S, false, true>(a, j, v, cur, g);
+          if (j < jfull)
+            seg_forward<S, true>(a, j, cur, g, xs, u0, changed, fl, lane);
+          else
+            seg_forward<S, false>(a, j, cur, g, xs, u0, changed, fl, lane);
+          double lam[3];
+          lam[0] = fma(ve.p00, xs[0], fma(ve.p01, xs[1], ve.p02 * xs[2])) - ve.s0;
+          lam[1] = fma(ve.p01, xs[0], fma(ve.p11, xs[1], ve.p12 * xs[2])) - ve.s1;
+          lam[2] = fma(ve.p02, xs[0], fma(ve.p12, xs[1], ve.p22 * xs[2])) - ve.s2;
+          if (j < jfull)
+            seg_costate<S, true>(a, j, cur, g, lam, changed, fl, lane);
+          else
+            seg_costate<S, false>(a, j, cur, g, lam, changed, fl, lane);
+          cur = nxt;
+          v = vn;
+        }
+        ++it;
+        if (!changed) {
+          conv = true;
+        } else if (it >= LQ_MAXIT) {
+          conv = true;
+          fq |= ZMPC_ST_MAXITER;
+        }
+      }
+    }
+    u0 = u0 / a.Tcu;  // v0 = T³ u0
+    if (valid) {
+      // state advance in the reference form x⁺ = A x + B u0 (zmp_controller.py:199)
+      double xn[3];
+      xn[0] = x[0] + a.T * x[1] + a.T2 * x[2] + a.T3 * u0;
+      xn[1] = x[1] + a.T * x[2] + a.T2 * u0;
+      xn[2] = x[2] + a.T * u0;
+      if (i == kstep) xn[1] -= kv;  // force kick (zmp_controller.py:90,105-106)
+      if (!(isfinite(xn[0]) && isfinite(xn[1]) && isfinite(xn[2]))) fq |= ZMPC_ST_NONFINITE;
+      x[0] = xn[0];
+      x[1] = xn[1];
+      x[2] = xn[2];
+      double* h = a.window_mode ? a.out + b * 3 : a.out + ((b * a.n + i + 1) * 2 + axis) * 3;
+      h[0] = xn[0];
+      h[1] = xn[1];
+      h[2] = xn[2];
+    }
+  }
+  if (valid && a.status != nullptr) {
+    if (a.window_mode)
+      a.status[b] = fq;
+    else if (fq != 0)
+      atomicOr(&a.status[b], fq);
+  }
+  if (a.dbg) {
+    if (lane == 0) atomicAdd(a.dbg + 0, n_wave_pass);
+    for (int o = 32; o > 0; o >>= 1) n_lane_pass += __shfl_xor(n_lane_pass, o);
+    if (lane == 0) atomicAdd(a.dbg + 1, n_lane_pass);
+  }
+}
+
+// Stage bounds into the kernel's tiled layout: source element (b, t, axis) at
+// b·sb + min(t, nsrc − 1)·st + axis·sa → dst[((axis·G + b/64)·rows + t)·64 + b%64] for t < rows.
+// 64 walks × 32 rows per workgroup through LDS; consecutive threads read consecutive source
+// elements for the walk-contiguous [B, n, 2] layout and write consecutive destination ones.
+struct StageArgs {
+  const double* src;
+  int64_t sb, st, sa, nsrc;
+  int64_t B, G, rows;
+  int naxes;
+  double* dst;
+};
+
+__global__ void __launch_bounds__(256) zmpc_bounds_stage_kernel(StageArgs s) {
+  __shared__ double tile[2][32][65];
+  const int64_t t0 = (int64_t)blockIdx.x * 32;
+  const int64_t b0 = (int64_t)blockIdx.y * 64;
+  const int per_walk = 32 * s.naxes;
+  for (int idx = threadIdx.x; idx < 64 * per_walk; idx += 256) {
+    const int w = idx / per_walk, rem = idx - w * per_walk;
+    const int tt = rem / s.naxes, ax = rem - tt * s.naxes;
+    const int64_t b = b0 + w;
+    int64_t t = t0 + tt;
+    if (t > s.nsrc - 1) t = s.nsrc - 1;  // window padding (zmp_controller.py:81-88)
+    double v = 0.0;
+    if (b < s.B) v = s.src[b * s.sb + t * s.st + ax * s.sa];
+    tile[ax][tt][w] = v;
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < 64 * per_walk; idx += 256) {
+    const int l = idx & 63, r = idx >> 6;
+    const int ax = r / 32, tt = r - ax * 32;
+    const int64_t t = t0 + tt;
+    if (t < s.rows)
+      s.dst[((ax * s.G + (b0 >> 6)) * s.rows + t) * 64 + l] = tile[ax][tt][l];
+  }
+}
+
+hipError_t stage(const double* src, int64_t sb, int64_t st, int64_t sa, int64_t nsrc, int64_t B,
+                 int64_t rows, int naxes, double* dst, hipStream_t s) {
+  StageArgs g{src, sb, st, sa, nsrc, B, (B + 63) / 64, rows, naxes, dst};
+  const dim3 grid((unsigned)((rows + 31) / 32), (unsigned)g.G);
+  hipLaunchKernelGGL(zmpc_bounds_stage_kernel, grid, dim3(256), 0, s, g);
+  return hipGetLastError();
+}
+
+// Kernel variant: Riccati steps per segment S × waves per SIMD W (ZMPC_STRICT_LQ="SxW",
+// A/B only; default below).
+struct LqVariant {
+  int S, W;
+};
+
+LqVariant lq_variant() {
+  static LqVariant v = [] {
+    LqVariant d{8, 1};
+    const char* e = getenv("ZMPC_STRICT_LQ");
+    if (e) {
+      int s = 0, w = 0;
+      if (sscanf(e, "%dx%d", &s, &w) == 2 && (s == 4 || s == 8) && (w == 1 || w == 2))
+        d = LqVariant{s, w};
+    }
+    return d;
+  }();
+  return v;
+}
+
+void fill_consts(const zmpc_plan* p, LqArgs& a) {
+  const int S = lq_variant().S;
+  a.N = p->N;
+  a.NS = (p->N + S - 1) / S;
+  a.T = p->T;
+  a.T2 = p->T2_2;
+  a.T3 = p->T3_6;
+  a.Tsq = p->T * p->T;
+  a.Tcu = a.Tsq * p->T;
+  const double hgt = p->hg / a.Tsq;
+  a.gam = 0.5 - hgt;
+  a.pi = 1.0 / 6.0 - hgt;  // p(0)/T³ (zmp_controller.py:171, i = j)
+  a.ipi = 1.0 / a.pi;
+  a.rho = p->R / (p->Q * a.Tcu * a.Tcu);
+  a.quu0 = a.pi * a.pi + a.rho;
+  a.gipi = a.gam / a.pi;
+  a.gam2 = a.gam * a.gam;
+  a.pig = a.pi * a.gam;
+  a.tolnu = 1e-13 / p->Q;
+}
+
+hipError_t launch_lq(LqArgs& a, int64_t waves, hipStream_t s) {
+  static const bool dbg_on = getenv("ZMPC_DEBUG_STRICT") != nullptr;  // diagnostics only
+  static unsigned long long* dbgbuf = nullptr;
+  if (dbg_on && !dbgbuf) (void)hipMalloc((void**)&dbgbuf, 8 * sizeof(unsigned long long));
+  if (dbg_on && dbgbuf) {
+    (void)hipMemsetAsync(dbgbuf, 0, 8 * sizeof(unsigned long long), s);
+    a.dbg = dbgbuf;
+  }
+  const LqVariant var = lq_variant();
+  const int64_t blocks = (waves + LQ_WAVES - 1) / LQ_WAVES;
+  const size_t lds = (size_t)LQ_WAVES * a.NS * var.S * 64;
+  void (*k)(LqArgs) = var.S == 4 ? (var.W == 2 ? zmpc_strict_lq_kernel<4, 2>
+                                                : zmpc_strict_lq_kernel<4, 1>)
+                                 : (var.W == 2 ? zmpc_strict_lq_kernel<8, 2>
+                                               : zmpc_strict_lq_kernel<8, 1>);
+  hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(64 * LQ_WAVES), lds, s, a);
+  hipError_t e = hipGetLastError();
+  if (dbg_on && dbgbuf && e == hipSuccess) {
+    unsigned long long h[8];
+    (void)hipStreamSynchronize(s);
+    (void)hipMemcpy(h, dbgbuf, sizeof(h), hipMemcpyDeviceToHost);
+    fprintf(stderr, "[zmpc strict-lq dbg] waves=%lld wave_passes=%llu lane_passes=%llu\n",
+            (long long)waves, h[0], h[1]);
+  }
+  return e;
+}
+
+}  // namespace
+
+hipError_t zmpc_strict_lq_set_attrs() {
+  hipError_t e = hipSuccess;
+  const void* ks[] = {(const void*)zmpc_strict_lq_kernel<4, 1>,
+                      (const void*)zmpc_strict_lq_kernel<4, 2>,
+                      (const void*)zmpc_strict_lq_kernel<8, 1>,
+                      (const void*)zmpc_strict_lq_kernel<8, 2>};
+  for (const void* k : ks)
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  return e;
+}
+
+bool zmpc_strict_lq_supported(const zmpc_plan* p) {
+  const size_t rows = (size_t)(p->N + 7) / 8 * 8;
+  return p->N >= 1 && (size_t)LQ_WAVES * rows * 64 <= 160 * 1024;
+}
+
+hipError_t zmpc_launch_rollout_strict_lq(const zmpc_plan* p, int64_t B, int64_t n,
+                                         const double* zmax, const double* zmin,
+                                         int64_t bstride, const double* x0, const double* kick,
+                                         int64_t kick_step, const int64_t* kick_steps,
+                                         double* hist, int32_t* status, hipStream_t s,
+                                         std::string* why) {
+  LqArgs a{};
+  fill_consts(p, a);
+  a.window_mode = 0;
+  a.toff = 1;
+  a.n = n;
+  a.nsteps = n - 1;
+  a.B = B;
+  a.x0 = x0;
+  a.kick = kick;
+  a.kick_step = kick_step;
+  a.kick_steps = kick_steps;
+  a.out = hist;
+  a.status = status;
+  hipError_t e = hipSuccess;
+  if (status && (e = hipMemsetAsync(status, 0, sizeof(int32_t) * B, s)) != hipSuccess) return e;
+  const int64_t waves = 2 * ((B + 63) / 64);
+  // workspace: checkpoints + the staged bounds (rows past n − 1: the padded windows)
+  a.shared = bstride == 0 ? 1 : 0;
+  const int64_t Bst = a.shared ? 64 : B;  // a shared CoP is staged once, 64 identical lanes
+  a.groups = (Bst + 63) / 64;
+  a.rows = n + (int64_t)a.NS * lq_variant().S;  // the last segment reads up to NS·S − 1 ahead
+  const size_t ck_doubles = (size_t)waves * a.NS * 9 * 64;
+  const size_t st_doubles = (size_t)2 * a.groups * a.rows * 64;
+  double* ws = nullptr;
+  if ((e = hipMallocAsync((void**)&ws, (ck_doubles + 2 * st_doubles) * sizeof(double), s)) !=
+      hipSuccess) {
+    *why = std::string("strict workspace allocation: ") + hipGetErrorString(e);
+    return e;
+  }
+  a.ck = ws;
+  double* tmax = ws + ck_doubles;
+  double* tmin = tmax + st_doubles;
+  e = stage(zmax, bstride, 2, 1, n, Bst, a.rows, 2, tmax, s);
+  if (e == hipSuccess) e = stage(zmin, bstride, 2, 1, n, Bst, a.rows, 2, tmin, s);
+  a.zmax = tmax;
+  a.zmin = tmin;
+  if (e == hipSuccess) e = launch_lq(a, waves, s);
+  hipError_t ef = hipFreeAsync(ws, s);
+  return e != hipSuccess ? e : ef;
+}
+
+hipError_t zmpc_launch_step_strict_lq(const zmpc_plan* p, int64_t B, const double* x,
+                                      const double* zmax_win, const double* zmin_win,
+                                      double* x_next, int32_t* status, hipStream_t s,
+                                      std::string* why) {
+  LqArgs a{};
+  fill_consts(p, a);
+  a.window_mode = 1;
+  a.toff = 0;
+  a.n = p->N;
+  a.nsteps = 1;
+  a.B = B;
+  a.x0 = x;
+  a.kick = nullptr;
+  a.kick_step = -1;
+  a.out = x_next;
+  a.status = status;
+  a.shared = 0;
+  a.groups = (B + 63) / 64;
+  a.rows = (int64_t)a.NS * lq_variant().S;
+  const int64_t waves = (B + 63) / 64;
+  const size_t ck_doubles = (size_t)waves * a.NS * 9 * 64;
+  const size_t st_doubles = (size_t)a.groups * a.rows * 64;
+  double* ws = nullptr;
+  hipError_t e = hipMallocAsync((void**)&ws, (ck_doubles + 2 * st_doubles) * sizeof(double), s);
+  if (e != hipSuccess) {
+    *why = std::string("strict workspace allocation: ") + hipGetErrorString(e);
+    return e;
+  }
+  a.ck = ws;
+  double* tmax = ws + ck_doubles;
+  double* tmin = tmax + st_doubles;
+  e = stage(zmax_win, p->N, 1, 0, p->N, B, a.rows, 1, tmax, s);
+  if (e == hipSuccess) e = stage(zmin_win, p->N, 1, 0, p->N, B, a.rows, 1, tmin, s);
+  a.zmax = tmax;
+  a.zmin = tmin;
+  if (e == hipSuccess) e = launch_lq(a, waves, s);
+  hipError_t ef = hipFreeAsync(ws, s);
+  return e != hipSuccess ? e : ef;
+}

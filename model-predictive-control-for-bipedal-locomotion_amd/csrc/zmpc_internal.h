@@ -76,6 +76,20 @@ hipError_t zmpc_launch_step_strict(const zmpc_plan* p, int64_t B, const double* 
                                    double* x_next, int32_t* status, hipStream_t s,
                                    std::string* why);
 
+// strict box-QP in LQ form, one instance per lane (strict_lq.hip); the default strict path
+hipError_t zmpc_launch_rollout_strict_lq(const zmpc_plan* p, int64_t B, int64_t n,
+                                         const double* zmax, const double* zmin,
+                                         int64_t bstride, const double* x0, const double* kick,
+                                         int64_t kick_step, const int64_t* kick_steps,
+                                         double* hist, int32_t* status, hipStream_t s,
+                                         std::string* why);
+hipError_t zmpc_launch_step_strict_lq(const zmpc_plan* p, int64_t B, const double* x,
+                                      const double* zmax_win, const double* zmin_win,
+                                      double* x_next, int32_t* status, hipStream_t s,
+                                      std::string* why);
+bool zmpc_strict_lq_supported(const zmpc_plan* p);
+hipError_t zmpc_strict_lq_set_attrs();
+
 hipError_t zmpc_rollout_unc_set_attrs();
 hipError_t zmpc_strict_set_attrs();
 
