@@ -119,7 +119,10 @@ __device__ __forceinline__ void ric_step(const LqArgs& a, Ric& v, double hi, dou
   const double nqx1 = r + (v.s0 + v.s1);
   const double nqx2 = fma(a.gam, r, fma(h, v.s0, v.s1 + v.s2));
   const bool act = f != 0;
-  const double iq = 1.0 / Quu;
+  // 1/Quu: hardware reciprocal + two Newton steps (Quu ≥ ρ + π² > 0, no special cases)
+  double iq = __builtin_amdgcn_rcp(Quu);
+  iq = fma(iq, fma(-Quu, iq, 1.0), iq);
+  iq = fma(iq, fma(-Quu, iq, 1.0), iq);
   const double t = (f == 1) ? hi : lo;
   K0 = act ? a.ipi : ux0 * iq;
   K1 = act ? a.ipi : ux1 * iq;
@@ -291,7 +294,7 @@ __device__ __forceinline__ void ck_load(const double* ck, int j, Ric& v, int lan
   v.s2 = p[512];
 }
 
-template <int S, int W>
+template <int S, int W, bool PF>
 __global__ void __launch_bounds__(64 * LQ_WAVES, W) zmpc_strict_lq_kernel(LqArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lq_smem[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -367,27 +370,35 @@ __global__ void __launch_bounds__(64 * LQ_WAVES, W) zmpc_strict_lq_kernel(LqArgs
         SegOut<S> g;
         // sweep A: full backward Riccati, checkpoints at segment boundaries; the next
         // segment's loads are in flight under the current segment's recursion
-        seg_load(a, a.NS - 1, L, i, fl, cur);
+        if (PF) seg_load(a, a.NS - 1, L, i, fl, cur);
 #pragma unroll 1
         for (int j = a.NS - 1; j >= 0; --j) {
-          if (j > 0) seg_load(a, j - 1, L, i, fl, nxt);
+          if (!PF)
+            seg_load(a, j, L, i, fl, cur);
+          else if (j > 0)
+            seg_load(a, j - 1, L, i, fl, nxt);
           ck_store(a, ck, j, v, lane);
           if (j < jfull)
             seg_riccati<S, true, false>(a, j, v, cur, g);
           else
             seg_riccati<S, false, false>(a, j, v, cur, g);
-          cur = nxt;
+          if (PF) cur = nxt;
         }
         // sweep B: per segment from the front — recompute its Riccati steps from the
         // checkpoint, forward, then the costate back through it from λ at its end
         double xs[3] = {x[0], a.T * x[1], a.Tsq * x[2]};  // ξ
         bool changed = false;
-        seg_load(a, 0, L, i, fl, cur);
         Ric vn;
-        ck_load(ck, 0, v, lane);
+        if (PF) {
+          seg_load(a, 0, L, i, fl, cur);
+          ck_load(ck, 0, v, lane);
+        }
 #pragma unroll 1
         for (int j = 0; j < a.NS; ++j) {
-          if (j + 1 < a.NS) {
+          if (!PF) {
+            seg_load(a, j, L, i, fl, cur);
+            ck_load(ck, j, v, lane);
+          } else if (j + 1 < a.NS) {
             seg_load(a, j + 1, L, i, fl, nxt);
             ck_load(ck, j + 1, vn, lane);
           }
@@ -408,8 +419,10 @@ __global__ void __launch_bounds__(64 * LQ_WAVES, W) zmpc_strict_lq_kernel(LqArgs
             seg_costate<S, true>(a, j, cur, g, lam, changed, fl, lane);
           else
             seg_costate<S, false>(a, j, cur, g, lam, changed, fl, lane);
-          cur = nxt;
-          v = vn;
+          if (PF) {
+            cur = nxt;
+            v = vn;
+          }
         }
         ++it;
         if (!changed) {
@@ -504,7 +517,7 @@ struct LqVariant {
 
 LqVariant lq_variant() {
   static LqVariant v = [] {
-    LqVariant d{8, 1};
+    LqVariant d{8, 2};
     const char* e = getenv("ZMPC_STRICT_LQ");
     if (e) {
       int s = 0, w = 0;
@@ -548,10 +561,10 @@ hipError_t launch_lq(LqArgs& a, int64_t waves, hipStream_t s) {
   const LqVariant var = lq_variant();
   const int64_t blocks = (waves + LQ_WAVES - 1) / LQ_WAVES;
   const size_t lds = (size_t)LQ_WAVES * a.NS * var.S * 64;
-  void (*k)(LqArgs) = var.S == 4 ? (var.W == 2 ? zmpc_strict_lq_kernel<4, 2>
-                                                : zmpc_strict_lq_kernel<4, 1>)
-                                 : (var.W == 2 ? zmpc_strict_lq_kernel<8, 2>
-                                               : zmpc_strict_lq_kernel<8, 1>);
+  void (*k)(LqArgs) = var.S == 4 ? (var.W == 2 ? zmpc_strict_lq_kernel<4, 2, false>
+                                                : zmpc_strict_lq_kernel<4, 1, true>)
+                                 : (var.W == 2 ? zmpc_strict_lq_kernel<8, 2, false>
+                                               : zmpc_strict_lq_kernel<8, 1, true>);
   hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(64 * LQ_WAVES), lds, s, a);
   hipError_t e = hipGetLastError();
   if (dbg_on && dbgbuf && e == hipSuccess) {
@@ -568,10 +581,10 @@ hipError_t launch_lq(LqArgs& a, int64_t waves, hipStream_t s) {
 
 hipError_t zmpc_strict_lq_set_attrs() {
   hipError_t e = hipSuccess;
-  const void* ks[] = {(const void*)zmpc_strict_lq_kernel<4, 1>,
-                      (const void*)zmpc_strict_lq_kernel<4, 2>,
-                      (const void*)zmpc_strict_lq_kernel<8, 1>,
-                      (const void*)zmpc_strict_lq_kernel<8, 2>};
+  const void* ks[] = {(const void*)zmpc_strict_lq_kernel<4, 1, true>,
+                      (const void*)zmpc_strict_lq_kernel<4, 2, false>,
+                      (const void*)zmpc_strict_lq_kernel<8, 1, true>,
+                      (const void*)zmpc_strict_lq_kernel<8, 2, false>};
   for (const void* k : ks)
     if (e == hipSuccess)
       e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
