@@ -45,6 +45,7 @@ struct LqArgs {
   int N, NS;             // horizon, segments ⌈N/S⌉
   int toff;              // window slot k reads time i + toff + k (1 rollout, 0 step)
   int window_mode;
+  int drift;             // max timesteps a lane may run ahead of its wave's slowest lane
   int64_t n;             // samples per walk (rollout; 1 in window mode)
   int64_t nsteps;        // timesteps (n − 1, or 1)
   int64_t B;             // walks (rollout) or instances (step)
@@ -90,6 +91,7 @@ template <int S>
 struct SegOut {  // a segment's feedback (u = −K x − kff) and forward outputs, per step
   double K0[S], K1[S], K2[S], kf[S];
   double w[S];  // forward: Q (z_k − r_k) at free slots, u_k at active slots
+  int nf[S];     // forward: the free slots' primal verdict (0 stays free, 1/2 violated)
 };
 
 // One backward Riccati step in scaled coordinates (see header and LqArgs).  Inputs: V_{k+1}
@@ -160,7 +162,8 @@ struct Lane {
 template <int S>
 __device__ __forceinline__ void seg_load(const LqArgs& a, int j, const Lane& L, int64_t i,
                                          const unsigned char* fl, SegIn<S>& in) {
-  // segment's first row (uniform); the S rows are 512 B apart: one base, immediate offsets
+  // segment's first row (the lane's own timestep); its S rows are 512 B apart: one address,
+  // immediate offsets
   const int64_t row0 = i + a.toff + (int64_t)j * S;
   const double* hp = L.hi + row0 * 64;
   const double* lp = L.lo + row0 * 64;
@@ -222,13 +225,7 @@ __device__ __forceinline__ void seg_forward(const LqArgs& a, int j, const SegIn<
       const double hi = in.hi[q], lo = in.lo[q];
       const double r = (hi + lo) / 2;
       g.w[q] = (f == 0) ? z - r : u;
-      if (f == 0) {
-        const int nf = (z > hi + tol) ? 1 : ((z < lo - tol) ? 2 : 0);
-        if (nf != 0) {
-          fl[k * 64 + lane] = (unsigned char)nf;
-          changed = true;
-        }
-      }
+      g.nf[q] = (z > hi + tol) ? 1 : ((z < lo - tol) ? 2 : 0);
     }
   }
 }
@@ -249,14 +246,15 @@ __device__ __forceinline__ void seg_costate(const LqArgs& a, int j, const SegIn<
       const double bl = fma(s6, lam[0], fma(h, lam[1], lam[2]));  // B̂ᵀλ_{k+1}
       // active: π e + ρ v + B̂ᵀλ_{k+1} = 0 (stationarity in v_k)
       const double e = (f == 0) ? g.w[q] : -fma(a.rho, g.w[q], bl) * a.ipi;
-      if (f != 0) {
+      {
         const double r = (hi + lo) / 2;
         const double t = (f == 1) ? hi : lo;
-        const double nu = e - (t - r);  // ν / Q
-        if ((f == 1 && nu < -a.tolnu) || (f == 2 && nu > a.tolnu)) {
-          fl[k * 64 + lane] = 0;
-          changed = true;
-        }
+        const double nu = e - (t - r);  // ν / Q (meaningful at active slots only)
+        const bool rel = (f == 1 && nu < -a.tolnu) || (f == 2 && nu > a.tolnu);
+        // the slot's new flag, written unconditionally (branch-free)
+        const int nf = (f == 0) ? g.nf[q] : (rel ? 0 : f);
+        fl[k * 64 + lane] = (unsigned char)nf;
+        changed |= nf != f;
       }
       const double l0 = lam[0], l1 = lam[1], l2 = lam[2];
       lam[0] = e + l0;
@@ -346,30 +344,29 @@ __global__ void __launch_bounds__(64 * LQ_WAVES, W) zmpc_strict_lq_kernel(LqArgs
           : -1;
   const double kv = (kstep >= 0) ? a.kick[b] : 0.0;
 
-  for (int64_t i = 0; i < a.nsteps; ++i) {
-    if (i > 0) {
-      // warm start: the previous set shifted one slot towards the present (slot N−1 kept)
-      const int bytes = (N - 1) * 64;
-      for (int c = 0; c < bytes; c += 1024) {
-        const int o = c + lane * 16;
-        if (o < bytes) {
-          const uint4 vv = *reinterpret_cast<const uint4*>(fl + o + 64);
-          *reinterpret_cast<uint4*>(fl + o) = vv;
-        }
-      }
-    }
-    bool conv = !valid;
-    int it = 0;
-    double u0 = 0.0;
-    while (__any(!conv)) {
-      ++n_wave_pass;
-      if (!conv) {
-        ++n_lane_pass;
+  // Each lane walks its own timestep i: a pass runs for every lane still inside its rollout;
+  // a lane whose working set repeated advances (state, history, shifted warm start) while the
+  // others keep iterating, so a wave's passes ≈ the slowest lane's total, not the per-timestep
+  // max.  The lanes stay within a few timesteps of each other: their bound reads touch a few
+  // 512-byte rows per slot.
+  int64_t i = 0;
+  bool active = valid && a.nsteps > 0;
+  int it = 0;
+  while (__any(active)) {
+    ++n_wave_pass;
+    // bounded drift: a lane more than `drift` timesteps ahead of the slowest waits, so a
+    // slot's bound loads stay within a few rows (lanes at the same row share 512-byte lines)
+    int imin = active ? (int)i : 0x7fffffff;
+    for (int o = 32; o > 0; o >>= 1) imin = min(imin, __shfl_xor(imin, o));
+    if (active && i <= (int64_t)imin + a.drift) {
+      ++n_lane_pass;
+      double u0 = 0.0;
+      bool changed = false;
+      {
         Ric v{0, 0, 0, 0, 0, 0, 0, 0, 0};
         SegIn<S> cur, nxt;
         SegOut<S> g;
-        // sweep A: full backward Riccati, checkpoints at segment boundaries; the next
-        // segment's loads are in flight under the current segment's recursion
+        // sweep A: full backward Riccati, checkpoints at segment boundaries
         if (PF) seg_load(a, a.NS - 1, L, i, fl, cur);
 #pragma unroll 1
         for (int j = a.NS - 1; j >= 0; --j) {
@@ -387,7 +384,6 @@ __global__ void __launch_bounds__(64 * LQ_WAVES, W) zmpc_strict_lq_kernel(LqArgs
         // sweep B: per segment from the front — recompute its Riccati steps from the
         // checkpoint, forward, then the costate back through it from λ at its end
         double xs[3] = {x[0], a.T * x[1], a.Tsq * x[2]};  // ξ
-        bool changed = false;
         Ric vn;
         if (PF) {
           seg_load(a, 0, L, i, fl, cur);
@@ -424,31 +420,39 @@ __global__ void __launch_bounds__(64 * LQ_WAVES, W) zmpc_strict_lq_kernel(LqArgs
             v = vn;
           }
         }
-        ++it;
-        if (!changed) {
-          conv = true;
-        } else if (it >= LQ_MAXIT) {
-          conv = true;
-          fq |= ZMPC_ST_MAXITER;
+      }
+      ++it;
+      if (changed && it >= LQ_MAXIT) {
+        fq |= ZMPC_ST_MAXITER;
+        changed = false;
+      }
+      if (!changed) {
+        // converged: advance in the reference form x⁺ = A x + B u0 (zmp_controller.py:199)
+        u0 = u0 / a.Tcu;  // v0 = T³ u0
+        double xn[3];
+        xn[0] = x[0] + a.T * x[1] + a.T2 * x[2] + a.T3 * u0;
+        xn[1] = x[1] + a.T * x[2] + a.T2 * u0;
+        xn[2] = x[2] + a.T * u0;
+        if (i == kstep) xn[1] -= kv;  // force kick (zmp_controller.py:90,105-106)
+        if (!(isfinite(xn[0]) && isfinite(xn[1]) && isfinite(xn[2]))) fq |= ZMPC_ST_NONFINITE;
+        x[0] = xn[0];
+        x[1] = xn[1];
+        x[2] = xn[2];
+        double* h = a.window_mode ? a.out + b * 3 : a.out + ((b * a.n + i + 1) * 2 + axis) * 3;
+        h[0] = xn[0];
+        h[1] = xn[1];
+        h[2] = xn[2];
+        ++i;
+        it = 0;
+        if (i < a.nsteps) {
+          // warm start: the converged set shifted one slot towards the present (slot N−1
+          // kept), this lane's column only
+#pragma unroll 8
+          for (int k = 0; k < N - 1; ++k) fl[k * 64 + lane] = fl[(k + 1) * 64 + lane];
+        } else {
+          active = false;
         }
       }
-    }
-    u0 = u0 / a.Tcu;  // v0 = T³ u0
-    if (valid) {
-      // state advance in the reference form x⁺ = A x + B u0 (zmp_controller.py:199)
-      double xn[3];
-      xn[0] = x[0] + a.T * x[1] + a.T2 * x[2] + a.T3 * u0;
-      xn[1] = x[1] + a.T * x[2] + a.T2 * u0;
-      xn[2] = x[2] + a.T * u0;
-      if (i == kstep) xn[1] -= kv;  // force kick (zmp_controller.py:90,105-106)
-      if (!(isfinite(xn[0]) && isfinite(xn[1]) && isfinite(xn[2]))) fq |= ZMPC_ST_NONFINITE;
-      x[0] = xn[0];
-      x[1] = xn[1];
-      x[2] = xn[2];
-      double* h = a.window_mode ? a.out + b * 3 : a.out + ((b * a.n + i + 1) * 2 + axis) * 3;
-      h[0] = xn[0];
-      h[1] = xn[1];
-      h[2] = xn[2];
     }
   }
   if (valid && a.status != nullptr) {
@@ -513,16 +517,30 @@ hipError_t stage(const double* src, int64_t sb, int64_t st, int64_t sa, int64_t 
 // A/B only; default below).
 struct LqVariant {
   int S, W;
+  bool PF;  // next segment's loads prefetched
+  void (*kernel)(LqArgs);
 };
 
+const LqVariant kLqVariants[] = {
+    {8, 2, false, zmpc_strict_lq_kernel<8, 2, false>},  // default
+    {8, 2, true, zmpc_strict_lq_kernel<8, 2, true>},
+    {8, 1, true, zmpc_strict_lq_kernel<8, 1, true>},
+    {4, 2, false, zmpc_strict_lq_kernel<4, 2, false>},
+    {4, 2, true, zmpc_strict_lq_kernel<4, 2, true>},
+    {4, 3, false, zmpc_strict_lq_kernel<4, 3, false>},
+};
+
+// ZMPC_STRICT_LQ="SxW" or "SxWp" (prefetch) picks a variant for A/B runs.
 LqVariant lq_variant() {
   static LqVariant v = [] {
-    LqVariant d{8, 2};
+    LqVariant d = kLqVariants[0];
     const char* e = getenv("ZMPC_STRICT_LQ");
     if (e) {
       int s = 0, w = 0;
-      if (sscanf(e, "%dx%d", &s, &w) == 2 && (s == 4 || s == 8) && (w == 1 || w == 2))
-        d = LqVariant{s, w};
+      char pf = 0;
+      const int got = sscanf(e, "%dx%d%c", &s, &w, &pf);
+      for (const LqVariant& c : kLqVariants)
+        if (got >= 2 && c.S == s && c.W == w && c.PF == (got == 3 && pf == 'p')) d = c;
     }
     return d;
   }();
@@ -548,6 +566,11 @@ void fill_consts(const zmpc_plan* p, LqArgs& a) {
   a.gam2 = a.gam * a.gam;
   a.pig = a.pi * a.gam;
   a.tolnu = 1e-13 / p->Q;
+  static const int drift = [] {
+    const char* e = getenv("ZMPC_STRICT_LQ_DRIFT");  // A/B only
+    return e ? atoi(e) : 2;
+  }();
+  a.drift = drift;
 }
 
 hipError_t launch_lq(LqArgs& a, int64_t waves, hipStream_t s) {
@@ -561,11 +584,7 @@ hipError_t launch_lq(LqArgs& a, int64_t waves, hipStream_t s) {
   const LqVariant var = lq_variant();
   const int64_t blocks = (waves + LQ_WAVES - 1) / LQ_WAVES;
   const size_t lds = (size_t)LQ_WAVES * a.NS * var.S * 64;
-  void (*k)(LqArgs) = var.S == 4 ? (var.W == 2 ? zmpc_strict_lq_kernel<4, 2, false>
-                                                : zmpc_strict_lq_kernel<4, 1, true>)
-                                 : (var.W == 2 ? zmpc_strict_lq_kernel<8, 2, false>
-                                               : zmpc_strict_lq_kernel<8, 1, true>);
-  hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(64 * LQ_WAVES), lds, s, a);
+  hipLaunchKernelGGL(var.kernel, dim3((unsigned)blocks), dim3(64 * LQ_WAVES), lds, s, a);
   hipError_t e = hipGetLastError();
   if (dbg_on && dbgbuf && e == hipSuccess) {
     unsigned long long h[8];
@@ -581,13 +600,10 @@ hipError_t launch_lq(LqArgs& a, int64_t waves, hipStream_t s) {
 
 hipError_t zmpc_strict_lq_set_attrs() {
   hipError_t e = hipSuccess;
-  const void* ks[] = {(const void*)zmpc_strict_lq_kernel<4, 1, true>,
-                      (const void*)zmpc_strict_lq_kernel<4, 2, false>,
-                      (const void*)zmpc_strict_lq_kernel<8, 1, true>,
-                      (const void*)zmpc_strict_lq_kernel<8, 2, false>};
-  for (const void* k : ks)
+  for (const LqVariant& c : kLqVariants)
     if (e == hipSuccess)
-      e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      e = hipFuncSetAttribute((const void*)c.kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              160 * 1024);
   return e;
 }
 
