@@ -50,6 +50,10 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 FP64_PEAK_TFS = 78.6    # FP64 vector = matrix peak (spec)
 FP64_SUSTAINED_TFS = 56.6  # profiles/r1_fp64_peak.log: register-only FMA chains, 8 waves/SIMD
 SEED = 20251226
+# strict_lq.hip FLOP per instance-slot of one active-set pass (fma = 2): working-set slot =
+# Riccati step 117 + forward 24 + costate 19; free-tail slot = s recursion 23 + forward 21
+STRICT_FLOP_WS = 160
+STRICT_FLOP_TAIL = 44
 
 
 CONFIGS = {
@@ -232,6 +236,8 @@ def main():
     for _ in range(args.warmup):
         launch()
     torch.cuda.synchronize()
+    if cfg.strict:
+        plan.counters(reset=True)  # count the timed launches only
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -252,6 +258,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1) / args.steps
+    work = plan.counters() if cfg.strict else None
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -265,7 +272,6 @@ def main():
     alg_bytes = 2 * (1 if wl["shared"] else B) * n * 2 * 8 + B * n * 6 * 8
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     flops = B * (n - 1) * 2 * (2 * cfg.horizon + 20)
-    gemm_tf = B * (n - 1) * 2 * 2 * cfg.horizon ** 2 / (kern_ms * 1e-3) / 1e12
     workload = (f"config{conf}" + ("_unc" if conf == 4 and not cfg.strict else "") +
                 f"_n{cfg.horizon}_b{B}")
 
@@ -346,12 +352,25 @@ def main():
                     "unit": "TFLOP/s", "frac": fp64_tfs / FP64_PEAK_TFS,
                     "engine": "FP64 VALU (v_mfma_f64 measured slower, DESIGN.md §4)"}
         else:
-            # strict: the per-step z-space GEMM D = G·W (2N² FLOP per solve) bounds it
-            roof = {"bound": "mfma", "achieved": gemm_tf, "peak": FP64_PEAK_TFS,
-                    "unit": "TFLOP/s", "frac": gemm_tf / FP64_PEAK_TFS}
+            # strict (strict_lq.hip): FP64 VALU-bound.  Algorithmic FLOPs = the executed
+            # active-set passes (kernel counters) x the minimal per-pass work: one backward
+            # Riccati + forward + costate per working-set slot, one s-recursion + forward per
+            # free-tail slot (the sweep-B recompute is not counted)
+            per = max(1, work["launches"])
+            slots = work["instance_passes"] * cfg.horizon
+            ws = work["working_set_slots"]
+            sflops = (ws * STRICT_FLOP_WS + (slots - ws) * STRICT_FLOP_TAIL) / per
+            s_tf = sflops / (kern_ms * 1e-3) / 1e12
+            roof = {"bound": "mfma", "achieved": s_tf, "peak": FP64_PEAK_TFS,
+                    "unit": "TFLOP/s", "frac": s_tf / FP64_PEAK_TFS,
+                    "engine": "FP64 VALU (one instance per lane; no MFMA-shaped work)",
+                    "strict_alg_flops_per_launch": sflops,
+                    "passes_per_solve": work["instance_passes"] / per / (B * (n - 1) * 2),
+                    "lane_efficiency": work["instance_passes"] / max(1, 64 * work["wave_passes"]),
+                    "working_set_slot_frac": ws / max(1, slots)}
         roof.update({
             "traffic": traffic,
-            "kernel": "zmpc_strict_kernel" if cfg.strict else "zmpc_rollout_unc_kernel",
+            "kernel": "zmpc_strict_lq_kernel" if cfg.strict else "zmpc_rollout_unc_kernel",
             "kernel_ms": kern_ms, "alg_bytes_per_launch": alg_bytes,
             "hbm_gbs": achieved, "alg_flops_per_launch": flops,
             "fp64_frac_alg": flops / (kern_ms * 1e-3) / (FP64_PEAK_TFS * 1e12),

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define ZMPC_ABI_VERSION 2
+#define ZMPC_ABI_VERSION 3
 
 /* return codes */
 #define ZMPC_OK 0
@@ -72,6 +72,22 @@ int zmpc_plan_destroy(zmpc_plan* plan);
  *       7 = Hz = Q·I + R·Pu⁻ᵀPu⁻¹ = G⁻¹ (N*N, strict plans only).
  * count = number of doubles dst can hold; must be >= the quantity's size. */
 int zmpc_plan_export(const zmpc_plan* plan, int32_t what, double* dst_host, int64_t count);
+
+/*
+ * Work counters of a strict plan's box-QP solver, summed over its zmpc_step / zmpc_rollout
+ * launches since creation or the last reset (diagnostics for the roofline accounting; the
+ * reference has no equivalent).  Copied to HOST memory after synchronising the plan's device:
+ *   [0] wave passes   (active-set passes of a 64-instance wave, lockstep)
+ *   [1] instance passes (active-set iterations summed over instances and timesteps)
+ *   [2] instance-slots through the working-set Riccati step (the rest of the
+ *       [1] x N instance-slots took the free-tail step)
+ *   [3] launches
+ * count = number of uint64 dst can hold (at most ZMPC_NCOUNTERS are written); reset != 0
+ * zeroes the counters after the copy.  A plan without strict workspace returns ZMPC_ESTATE.
+ * Since ABI 3.
+ */
+#define ZMPC_NCOUNTERS 4
+int zmpc_plan_counters(const zmpc_plan* plan, uint64_t* dst_host, int32_t count, int32_t reset);
 
 /*
  * Batched ZMPController.predict_wieber_axis (zmp_controller.py:149-201):

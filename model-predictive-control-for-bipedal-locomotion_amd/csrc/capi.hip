@@ -40,6 +40,8 @@ void free_plan(zmpc_plan* p) {
     if (b) (void)hipFree(b);
   if (p->info) (void)hipFree(p->info);
   if (p->scratch) (void)hipFree(p->scratch);
+  if (p->lqtab) (void)hipFree(p->lqtab);
+  if (p->lqcnt) (void)hipFree(p->lqcnt);
   delete p;
 }
 
@@ -127,12 +129,25 @@ int zmpc_plan_create(int device, int32_t N, double T, double T2_2, double T3_6, 
       free_plan(P);
       return fail(ZMPC_ENOMEM, std::string("hipMalloc scratch: ") + hipGetErrorString(e));
     }
+    if ((e = hipMalloc((void**)&P->lqtab, zmpc_strict_lq_table_doubles(N) * sizeof(double))) !=
+            hipSuccess ||
+        (e = hipMalloc((void**)&P->lqcnt, ZMPC_NCOUNTERS * sizeof(unsigned long long))) !=
+            hipSuccess) {
+      free_plan(P);
+      return fail(ZMPC_ENOMEM, std::string("hipMalloc strict table: ") + hipGetErrorString(e));
+    }
   }
   hipStream_t s = (hipStream_t)stream;
   (void)hipMemsetAsync(P->k, 0, ((size_t)P->Kpad + 64) * sizeof(double), s);
+  if (P->lqcnt)
+    (void)hipMemsetAsync(P->lqcnt, 0, ZMPC_NCOUNTERS * sizeof(unsigned long long), s);
   if ((e = zmpc_launch_plan(P, s)) != hipSuccess) {
     free_plan(P);
     return hip_fail(e, "plan kernels");
+  }
+  if (P->lqtab && (e = zmpc_strict_lq_build_table(P, s)) != hipSuccess) {
+    free_plan(P);
+    return hip_fail(e, "strict table kernel");
   }
   if ((e = hipStreamSynchronize(s)) != hipSuccess) {
     free_plan(P);
@@ -186,6 +201,26 @@ int zmpc_plan_export(const zmpc_plan* P, int32_t what, double* dst, int64_t coun
   if (e != hipSuccess) return hip_fail(e, "hipDeviceSynchronize");
   e = hipMemcpy(dst, src, n * sizeof(double), hipMemcpyDeviceToHost);
   if (e != hipSuccess) return hip_fail(e, "hipMemcpy");
+  return ZMPC_OK;
+}
+
+int zmpc_plan_counters(const zmpc_plan* P, uint64_t* dst, int32_t count, int32_t reset) {
+  g_err.clear();
+  if (!P || !dst) return fail(ZMPC_EINVAL, "NULL plan or destination");
+  if (count < 0) return fail(ZMPC_EINVAL, "count < 0");
+  if (!P->lqcnt) return fail(ZMPC_ESTATE, "plan has no strict solver counters");
+  DeviceGuard g(P->device);
+  if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
+  hipError_t e = hipDeviceSynchronize();
+  if (e != hipSuccess) return hip_fail(e, "hipDeviceSynchronize");
+  unsigned long long h[ZMPC_NCOUNTERS];
+  e = hipMemcpy(h, P->lqcnt, sizeof(h), hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return hip_fail(e, "hipMemcpy");
+  for (int i = 0; i < count && i < ZMPC_NCOUNTERS; ++i) dst[i] = (uint64_t)h[i];
+  if (reset) {
+    e = hipMemset(P->lqcnt, 0, sizeof(h));
+    if (e != hipSuccess) return hip_fail(e, "hipMemset");
+  }
   return ZMPC_OK;
 }
 

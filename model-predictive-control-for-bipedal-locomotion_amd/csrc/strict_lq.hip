@@ -22,24 +22,37 @@
 // solution are the same, at O(N) per pass instead of a reduced Cholesky.
 //
 // Mapping: a lane owns one instance (one walk, one axis) for the whole rollout; a wave holds
-// 64 walks of one axis, in time lockstep (a wave's passes per timestep = the max over its
-// lanes; converged lanes are masked off).  The bounds come in [axis][t][walk] (a staging
-// transpose), so a wave's load of one window slot is 512 contiguous bytes.  Per pass:
+// 64 walks of one axis.  The bounds come in [axis][t][walk] (a staging transpose), so a wave's
+// load of one window slot is 512 contiguous bytes.  Per pass:
 //   sweep A  backward Riccati over the horizon in segments of S steps, checkpointing (P, s)
 //            at segment boundaries to a per-lane global slab (coalesced [.., 9, 64]);
 //   sweep B  per segment from the front: reload its checkpoint, recompute its S Riccati
-//            steps into registers (K, kff, PB, Bᵀs, bounds, flags), roll forward through it,
-//            check primal/dual feasibility, update the slot flags (LDS, [N][64] bytes).
+//            steps into registers (K, kff, bounds, flags), roll forward through it, check
+//            primal/dual feasibility, update the slot flags (LDS, [N][64] bytes).
 // Everything a pass touches besides the bounds and the checkpoints lives in registers.
+//
+// Free structure.  The quadratic part P of the value function (with the gain K and 1/Quu)
+// depends on the working set only, never on the bounds.  Behind the last active slot of every
+// lane of a wave (the free tail) they are the plan's table (zmpc_strict_lq_build_table, the
+// same arithmetic), so a tail slot costs the linear recursion of s twice and the forward step
+// (≈70 FLOP instead of ≈280), with no flag loads and no costate.  In sweep A, a segment before
+// the tail in which no lane has an active slot runs the free form of the step (no per-lane
+// selects, no D).
+// The x axis of a walk is free almost everywhere; the y axis keeps active slots through most
+// of the horizon while the robot steps (scripts/strict_active_stats.py).
 #include <cstdio>
 #include <cstdlib>
 
 #include "zmpc_internal.h"
 
+#pragma clang fp contract(off)  // every fused multiply-add below is an explicit fma()
+
 namespace {
 
-constexpr int LQ_WAVES = 4;      // independent waves per workgroup
-constexpr int LQ_MAXIT = 64;     // active-set pass cap (as strict.hip)
+constexpr int LQ_WAVES = 4;   // independent waves per workgroup
+constexpr int LQ_MAXIT = 64;  // active-set pass cap (as strict.hip)
+constexpr int TAB = 16;       // doubles per slot of the free-tail table: [0..2] K, [3] 1/Quu,
+                              // [4..9] P after the slot (V_k: slots k..N−1 free), padding
 
 struct LqArgs {
   int N, NS;             // horizon, segments ⌈N/S⌉
@@ -64,7 +77,7 @@ struct LqArgs {
   double* out;           // rollout hist [B,n,2,3], step x_next [B,3]
   int32_t* status;
   double* ck;            // checkpoints [waves][NS][9][64]
-  unsigned long long* dbg;  // ZMPC_DEBUG_STRICT counters, null normally
+  unsigned long long* cnt;  // plan work counters (zmpc_plan_counters), may be null
   // LIPM / QP constants.  The passes run in scaled coordinates ξ = [x0, T x1, T² x2],
   // v = T³ u, objective divided by Q: Â = [[1,1,½],[0,1,1],[0,0,1]], B̂ = [⅙, ½, 1],
   // z = ĉᵀξ + π v with ĉ = [1, 1, γ], γ = ½ − (h/g)/T², π = ⅙ − (h/g)/T² (= p(0)/T³),
@@ -90,36 +103,37 @@ struct SegIn {  // a segment's window slots: bounds and working-set flags
 template <int S>
 struct SegOut {  // a segment's feedback (u = −K x − kff) and forward outputs, per step
   double K0[S], K1[S], K2[S], kf[S];
-  double w[S];  // forward: Q (z_k − r_k) at free slots, u_k at active slots
-  int nf[S];     // forward: the free slots' primal verdict (0 stays free, 1/2 violated)
+  double w[S];  // forward: z_k − r_k at free slots, u_k at active slots
+  int nf[S];    // forward: the free slots' primal verdict (0 stays free, 1/2 violated)
 };
 
-// One backward Riccati step in scaled coordinates (see header and LqArgs).  Inputs: V_{k+1}
-// in v, slot flag f, bounds.  Outputs the step's feedback v_k = −K ξ_k − kff.
+constexpr double kH = 0.5, kS6 = 1.0 / 6.0;
+
+// One backward Riccati step in scaled coordinates (see header and LqArgs), per-lane slot flag
+// f.  Inputs: V_{k+1} in v, bounds.  Outputs the step's feedback v_k = −K ξ_k − kff.
 __device__ __forceinline__ void ric_step(const LqArgs& a, Ric& v, double hi, double lo, int f,
                                          double& K0, double& K1, double& K2, double& kf) {
-  constexpr double h = 0.5, s6 = 1.0 / 6.0;
   // P B̂, B̂ᵀs, B̂ᵀPB̂
-  const double pb0 = fma(s6, v.p00, fma(h, v.p01, v.p02));
-  const double pb1 = fma(s6, v.p01, fma(h, v.p11, v.p12));
-  const double pb2 = fma(s6, v.p02, fma(h, v.p12, v.p22));
-  const double sb = fma(s6, v.s0, fma(h, v.s1, v.s2));
-  const double bpb = fma(s6, pb0, fma(h, pb1, pb2));
+  const double pb0 = fma(kS6, v.p00, fma(kH, v.p01, v.p02));
+  const double pb1 = fma(kS6, v.p01, fma(kH, v.p11, v.p12));
+  const double pb2 = fma(kS6, v.p02, fma(kH, v.p12, v.p22));
+  const double sb = fma(kS6, v.s0, fma(kH, v.s1, v.s2));
+  const double bpb = fma(kS6, pb0, fma(kH, pb1, pb2));
   // P Â (columns 1, 2) and ÂᵀPÂ
-  const double m01 = v.p00 + v.p01, m02 = fma(h, v.p00, v.p01 + v.p02);
-  const double m11 = v.p01 + v.p11, m12 = fma(h, v.p01, v.p11 + v.p12);
-  const double m22 = fma(h, v.p02, v.p12 + v.p22);
-  const double S11 = m01 + m11, S12 = m02 + m12, S22 = fma(h, m02, m12 + m22);
+  const double m01 = v.p00 + v.p01, m02 = fma(kH, v.p00, v.p01 + v.p02);
+  const double m11 = v.p01 + v.p11, m12 = fma(kH, v.p01, v.p11 + v.p12);
+  const double m22 = fma(kH, v.p02, v.p12 + v.p22);
+  const double S11 = m01 + m11, S12 = m02 + m12, S22 = fma(kH, m02, m12 + m22);
   // Qux = π ĉ + (PB̂)ᵀÂ, Quu, qu, −qx = r ĉ + Âᵀs
   const double ux0 = a.pi + pb0;
   const double ux1 = a.pi + (pb0 + pb1);
-  const double ux2 = a.pig + fma(h, pb0, pb1 + pb2);
+  const double ux2 = a.pig + fma(kH, pb0, pb1 + pb2);
   const double Quu = a.quu0 + bpb;
   const double r = (hi + lo) / 2;  // z_ref (zmp_controller.py:184)
   const double qu = -fma(a.pi, r, sb);
   const double nqx0 = r + v.s0;
   const double nqx1 = r + (v.s0 + v.s1);
-  const double nqx2 = fma(a.gam, r, fma(h, v.s0, v.s1 + v.s2));
+  const double nqx2 = fma(a.gam, r, fma(kH, v.s0, v.s1 + v.s2));
   const bool act = f != 0;
   // 1/Quu: hardware reciprocal + two Newton steps (Quu ≥ ρ + π² > 0, no special cases)
   double iq = __builtin_amdgcn_rcp(Quu);
@@ -151,15 +165,75 @@ __device__ __forceinline__ void ric_step(const LqArgs& a, Ric& v, double hi, dou
   v.p22 = P22;
 }
 
+// The same step for a free slot (ric_step with f = 0 and D = 0 folded: identical values up to
+// the sign of a zero).  Also returns 1/Quu (the free-tail table).
+__device__ __forceinline__ void ric_free(const LqArgs& a, Ric& v, double r, double& K0,
+                                         double& K1, double& K2, double& kf, double& iqo) {
+  const double pb0 = fma(kS6, v.p00, fma(kH, v.p01, v.p02));
+  const double pb1 = fma(kS6, v.p01, fma(kH, v.p11, v.p12));
+  const double pb2 = fma(kS6, v.p02, fma(kH, v.p12, v.p22));
+  const double sb = fma(kS6, v.s0, fma(kH, v.s1, v.s2));
+  const double bpb = fma(kS6, pb0, fma(kH, pb1, pb2));
+  const double m01 = v.p00 + v.p01, m02 = fma(kH, v.p00, v.p01 + v.p02);
+  const double m11 = v.p01 + v.p11, m12 = fma(kH, v.p01, v.p11 + v.p12);
+  const double m22 = fma(kH, v.p02, v.p12 + v.p22);
+  const double S11 = m01 + m11, S12 = m02 + m12, S22 = fma(kH, m02, m12 + m22);
+  const double ux0 = a.pi + pb0;
+  const double ux1 = a.pi + (pb0 + pb1);
+  const double ux2 = a.pig + fma(kH, pb0, pb1 + pb2);
+  const double Quu = a.quu0 + bpb;
+  const double qu = -fma(a.pi, r, sb);
+  const double nqx0 = r + v.s0;
+  const double nqx1 = r + (v.s0 + v.s1);
+  const double nqx2 = fma(a.gam, r, fma(kH, v.s0, v.s1 + v.s2));
+  double iq = __builtin_amdgcn_rcp(Quu);
+  iq = fma(iq, fma(-Quu, iq, 1.0), iq);
+  iq = fma(iq, fma(-Quu, iq, 1.0), iq);
+  K0 = ux0 * iq;
+  K1 = ux1 * iq;
+  K2 = ux2 * iq;
+  kf = qu * iq;
+  iqo = iq;
+  const double P00 = fma(-ux0, K0, 1.0 + v.p00);
+  const double P01 = fma(-ux0, K1, 1.0 + m01);
+  const double P02 = fma(-ux0, K2, a.gam + m02);
+  const double P11 = fma(-ux1, K1, 1.0 + S11);
+  const double P12 = fma(-ux1, K2, a.gam + S12);
+  const double P22 = fma(-ux2, K2, a.gam2 + S22);
+  v.s0 = fma(K0, qu, nqx0);
+  v.s1 = fma(K1, qu, nqx1);
+  v.s2 = fma(K2, qu, nqx2);
+  v.p00 = P00;
+  v.p01 = P01;
+  v.p02 = P02;
+  v.p11 = P11;
+  v.p12 = P12;
+  v.p22 = P22;
+}
+
+// A free-tail step: P, K and 1/Quu come from the table, only s moves (ric_free's s update).
+__device__ __forceinline__ void ric_tail(const LqArgs& a, Ric& v, double r, double K0, double K1,
+                                         double K2, double iq, double& kf) {
+  const double sb = fma(kS6, v.s0, fma(kH, v.s1, v.s2));
+  const double qu = -fma(a.pi, r, sb);
+  const double nqx0 = r + v.s0;
+  const double nqx1 = r + (v.s0 + v.s1);
+  const double nqx2 = fma(a.gam, r, fma(kH, v.s0, v.s1 + v.s2));
+  kf = qu * iq;
+  v.s0 = fma(K0, qu, nqx0);
+  v.s1 = fma(K1, qu, nqx1);
+  v.s2 = fma(K2, qu, nqx2);
+}
+
 struct Lane {
   const double* hi;  // wave's staged z_max rows (uniform)
   const double* lo;  // wave's staged z_min rows
   int lane;
 };
 
-// Issue the loads of segment j's slots (bounds, flags).  Slots past N are clamped to N − 1
-// (loaded, never used) so the loads carry no guards and can be issued a segment ahead.
-template <int S>
+// Issue the loads of segment j's slots (bounds, and the flags when FLAGS).  Slots past N read
+// padded rows (loaded, never used) so the loads carry no guards.
+template <int S, bool FLAGS>
 __device__ __forceinline__ void seg_load(const LqArgs& a, int j, const Lane& L, int64_t i,
                                          const unsigned char* fl, SegIn<S>& in) {
   // segment's first row (the lane's own timestep); its S rows are 512 B apart: one address,
@@ -172,13 +246,23 @@ __device__ __forceinline__ void seg_load(const LqArgs& a, int j, const Lane& L, 
   for (int q = 0; q < S; ++q) {
     in.hi[q] = hp[q * 64 + L.lane];
     in.lo[q] = lp[q * 64 + L.lane];
-    in.f[q] = fp[q * 64 + L.lane];
+    if (FLAGS) in.f[q] = fp[q * 64 + L.lane];
   }
+}
+
+// No lane taking part has an active slot in the segment (wave-uniform).
+template <int S>
+__device__ __forceinline__ bool seg_free(const SegIn<S>& in) {
+  int any = 0;
+#pragma unroll
+  for (int q = 0; q < S; ++q) any |= in.f[q];
+  return !__any(any != 0);
 }
 
 // Riccati steps of segment j (slots jS + S−1 down to jS).  KEEP: feedback kept in g (sweep
 // B) or dropped (sweep A).  FULL: every slot of the segment is < N (straight-line code).
-template <int S, bool FULL, bool KEEP>
+// FREE: no lane has an active slot here.
+template <int S, bool FULL, bool KEEP, bool FREE>
 __device__ __forceinline__ void seg_riccati(const LqArgs& a, int j, Ric& v, const SegIn<S>& in,
                                             SegOut<S>& g) {
 #pragma unroll
@@ -186,7 +270,12 @@ __device__ __forceinline__ void seg_riccati(const LqArgs& a, int j, Ric& v, cons
     const int k = j * S + q;
     if (FULL || k < a.N) {
       double K0, K1, K2, kf;
-      ric_step(a, v, in.hi[q], in.lo[q], in.f[q], K0, K1, K2, kf);
+      if (FREE) {
+        double iq;
+        ric_free(a, v, (in.hi[q] + in.lo[q]) / 2, K0, K1, K2, kf, iq);
+      } else {
+        ric_step(a, v, in.hi[q], in.lo[q], in.f[q], K0, K1, K2, kf);
+      }
       if (KEEP) {
         g.K0[q] = K0;
         g.K1[q] = K1;
@@ -200,13 +289,28 @@ __device__ __forceinline__ void seg_riccati(const LqArgs& a, int j, Ric& v, cons
   }
 }
 
+// Free-tail steps of segment j: the s recursion with the table's K and 1/Quu (kff kept in g
+// when KEEP).
+template <int S, bool FULL, bool KEEP>
+__device__ __forceinline__ void seg_tail(const LqArgs& a, const double* __restrict__ tab, int j,
+                                         Ric& v, const SegIn<S>& in, SegOut<S>& g) {
+#pragma unroll
+  for (int q = S - 1; q >= 0; --q) {
+    const int k = j * S + q;
+    if (FULL || k < a.N) {
+      const double* t = tab + (size_t)k * TAB;
+      double kf;
+      ric_tail(a, v, (in.hi[q] + in.lo[q]) / 2, t[0], t[1], t[2], t[3], kf);
+      if (KEEP) g.kf[q] = kf;
+    }
+  }
+}
+
 // Forward through segment j: roll the trajectory out (x advances to the segment's end),
 // primal check of the free slots, and the per-step input of the costate sweep.
 template <int S, bool FULL>
-__device__ __forceinline__ void seg_forward(const LqArgs& a, int j, const SegIn<S>& in, SegOut<S>& g,
-                                            double* x, double& u0, bool& changed,
-                                            unsigned char* fl, int lane) {
-  constexpr double h = 0.5, s6 = 1.0 / 6.0;
+__device__ __forceinline__ void seg_forward(const LqArgs& a, int j, const SegIn<S>& in,
+                                            SegOut<S>& g, double* x, double& u0) {
   const double tol = 1e-13;  // as strict.hip (tolz)
 #pragma unroll
   for (int q = 0; q < S; ++q) {
@@ -215,35 +319,64 @@ __device__ __forceinline__ void seg_forward(const LqArgs& a, int j, const SegIn<
       const double u = -fma(g.K0[q], x[0], fma(g.K1[q], x[1], g.K2[q] * x[2])) - g.kf[q];
       if (k == 0) u0 = u;
       const double z = fma(a.pi, u, fma(a.gam, x[2], x[0] + x[1]));
-      const double y0 = fma(s6, u, fma(h, x[2], x[0] + x[1]));
-      const double y1 = fma(h, u, x[1] + x[2]);
+      const double y0 = fma(kS6, u, fma(kH, x[2], x[0] + x[1]));
+      const double y1 = fma(kH, u, x[1] + x[2]);
       const double y2 = x[2] + u;
       x[0] = y0;
       x[1] = y1;
       x[2] = y2;
-      const int f = in.f[q];
       const double hi = in.hi[q], lo = in.lo[q];
       const double r = (hi + lo) / 2;
-      g.w[q] = (f == 0) ? z - r : u;
+      g.w[q] = (in.f[q] == 0) ? z - r : u;
       g.nf[q] = (z > hi + tol) ? 1 : ((z < lo - tol) ? 2 : 0);
     }
   }
 }
 
+// Forward through a free-tail segment (table K, kff from seg_tail): primal check and the new
+// flags (every slot here is free for every lane taking part, so no costate is needed).
+template <int S, bool FULL>
+__device__ __forceinline__ void seg_forward_tail(const LqArgs& a, const double* __restrict__ tab,
+                                                 int j, const SegIn<S>& in, const SegOut<S>& g,
+                                                 double* x, double& u0, bool& changed, int& kl,
+                                                 unsigned char* fl, int lane) {
+  const double tol = 1e-13;
+#pragma unroll
+  for (int q = 0; q < S; ++q) {
+    const int k = j * S + q;
+    if (FULL || k < a.N) {
+      const double* t = tab + (size_t)k * TAB;
+      const double u = -fma(t[0], x[0], fma(t[1], x[1], t[2] * x[2])) - g.kf[q];
+      if (k == 0) u0 = u;
+      const double z = fma(a.pi, u, fma(a.gam, x[2], x[0] + x[1]));
+      const double y0 = fma(kS6, u, fma(kH, x[2], x[0] + x[1]));
+      const double y1 = fma(kH, u, x[1] + x[2]);
+      const double y2 = x[2] + u;
+      x[0] = y0;
+      x[1] = y1;
+      x[2] = y2;
+      const int nf = (z > in.hi[q] + tol) ? 1 : ((z < in.lo[q] - tol) ? 2 : 0);
+      fl[k * 64 + lane] = (unsigned char)nf;
+      changed |= nf != 0;
+      kl = nf ? k : kl;
+    }
+  }
+}
+
 // Costate sweep back through segment j from λ at its end (λ_k = ∇V_k(x_k) = c1 e_k + Aᵀλ_{k+1},
-// e_k = Q (z_k − r_k) + ν_k): the bound multipliers ν_k of the active slots, dual check.
+// e_k = Q (z_k − r_k) + ν_k): the bound multipliers ν_k of the active slots, dual check, the
+// slot's new flag; kl = the last slot active in the new set.
 template <int S, bool FULL>
 __device__ __forceinline__ void seg_costate(const LqArgs& a, int j, const SegIn<S>& in,
                                             const SegOut<S>& g, double* lam, bool& changed,
-                                            unsigned char* fl, int lane) {
-  constexpr double h = 0.5, s6 = 1.0 / 6.0;
+                                            int& kl, unsigned char* fl, int lane) {
 #pragma unroll
   for (int q = S - 1; q >= 0; --q) {
     const int k = j * S + q;
     if (FULL || k < a.N) {
       const int f = in.f[q];
       const double hi = in.hi[q], lo = in.lo[q];
-      const double bl = fma(s6, lam[0], fma(h, lam[1], lam[2]));  // B̂ᵀλ_{k+1}
+      const double bl = fma(kS6, lam[0], fma(kH, lam[1], lam[2]));  // B̂ᵀλ_{k+1}
       // active: π e + ρ v + B̂ᵀλ_{k+1} = 0 (stationarity in v_k)
       const double e = (f == 0) ? g.w[q] : -fma(a.rho, g.w[q], bl) * a.ipi;
       {
@@ -255,25 +388,46 @@ __device__ __forceinline__ void seg_costate(const LqArgs& a, int j, const SegIn<
         const int nf = (f == 0) ? g.nf[q] : (rel ? 0 : f);
         fl[k * 64 + lane] = (unsigned char)nf;
         changed |= nf != f;
+        kl = (nf != 0 && k > kl) ? k : kl;
       }
       const double l0 = lam[0], l1 = lam[1], l2 = lam[2];
       lam[0] = e + l0;
       lam[1] = e + (l0 + l1);
-      lam[2] = fma(a.gam, e, fma(h, l0, l1 + l2));
+      lam[2] = fma(a.gam, e, fma(kH, l0, l1 + l2));
     }
   }
 }
 
-__device__ __forceinline__ void ck_store(const LqArgs& a, double* ck, int j, const Ric& v,
-                                         int lane) {
-  double* p = ck + (size_t)j * 9 * 64;
-  p += lane;
+// Sweep B through one working-set segment: Riccati from its checkpoint, forward, costate.
+template <int S, bool FULL>
+__device__ __forceinline__ void seg_sweep_b(const LqArgs& a, int j, Ric& v, const SegIn<S>& in,
+                                            SegOut<S>& g, double* xs, double& u0, bool& changed,
+                                            int& kl, unsigned char* fl, int lane) {
+  const Ric ve = v;  // V at the segment's end
+  seg_riccati<S, FULL, true, false>(a, j, v, in, g);
+  seg_forward<S, FULL>(a, j, in, g, xs, u0);
+  double lam[3];
+  lam[0] = fma(ve.p00, xs[0], fma(ve.p01, xs[1], ve.p02 * xs[2])) - ve.s0;
+  lam[1] = fma(ve.p01, xs[0], fma(ve.p11, xs[1], ve.p12 * xs[2])) - ve.s1;
+  lam[2] = fma(ve.p02, xs[0], fma(ve.p12, xs[1], ve.p22 * xs[2])) - ve.s2;
+  seg_costate<S, FULL>(a, j, in, g, lam, changed, kl, fl, lane);
+}
+
+__device__ __forceinline__ void ck_store(double* ck, int j, const Ric& v, int lane) {
+  double* p = ck + (size_t)j * 9 * 64 + lane;
   p[0] = v.p00;
   p[64] = v.p01;
   p[128] = v.p02;
   p[192] = v.p11;
   p[256] = v.p12;
   p[320] = v.p22;
+  p[384] = v.s0;
+  p[448] = v.s1;
+  p[512] = v.s2;
+}
+
+__device__ __forceinline__ void ck_store_s(double* ck, int j, const Ric& v, int lane) {
+  double* p = ck + (size_t)j * 9 * 64 + lane;
   p[384] = v.s0;
   p[448] = v.s1;
   p[512] = v.s2;
@@ -292,8 +446,16 @@ __device__ __forceinline__ void ck_load(const double* ck, int j, Ric& v, int lan
   v.s2 = p[512];
 }
 
-template <int S, int W, bool PF>
-__global__ void __launch_bounds__(64 * LQ_WAVES, W) zmpc_strict_lq_kernel(LqArgs a) {
+__device__ __forceinline__ void ck_load_s(const double* ck, int j, Ric& v, int lane) {
+  const double* p = ck + (size_t)j * 9 * 64 + lane;
+  v.s0 = p[384];
+  v.s1 = p[448];
+  v.s2 = p[512];
+}
+
+template <int S, int W>
+__global__ void __launch_bounds__(64 * LQ_WAVES, W)
+    zmpc_strict_lq_kernel(LqArgs a, const double* __restrict__ tab) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lq_smem[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int64_t gw = (int64_t)blockIdx.x * LQ_WAVES + wave;
@@ -337,87 +499,100 @@ __global__ void __launch_bounds__(64 * LQ_WAVES, W) zmpc_strict_lq_kernel(LqArgs
     }
   }
   int fq = 0;
-  unsigned long long n_wave_pass = 0, n_lane_pass = 0;
+  unsigned long long n_wave_pass = 0, n_lane_pass = 0, n_ws_slots = 0;
   const int64_t kstep =
       (!a.window_mode && axis == 1 && a.kick != nullptr && valid)
           ? (a.kick_steps ? a.kick_steps[b] : a.kick_step)
           : -1;
   const double kv = (kstep >= 0) ? a.kick[b] : 0.0;
 
-  // Each lane walks its own timestep i: a pass runs for every lane still inside its rollout;
-  // a lane whose working set repeated advances (state, history, shifted warm start) while the
-  // others keep iterating, so a wave's passes ≈ the slowest lane's total, not the per-timestep
-  // max.  The lanes stay within a few timesteps of each other: their bound reads touch a few
-  // 512-byte rows per slot.
+  // Each lane walks its own timestep i: a pass runs for every lane still inside its rollout
+  // and at most `drift` timesteps ahead of the wave's slowest lane (so a slot's bound loads
+  // stay within a few 512-byte rows); a lane whose working set repeated advances (state,
+  // history, shifted warm start) while the others keep iterating.
   int64_t i = 0;
   bool active = valid && a.nsteps > 0;
   int it = 0;
+  int klast = -1;  // last active slot of this lane's working set (−1: none)
   while (__any(active)) {
     ++n_wave_pass;
-    // bounded drift: a lane more than `drift` timesteps ahead of the slowest waits, so a
-    // slot's bound loads stay within a few rows (lanes at the same row share 512-byte lines)
     int imin = active ? (int)i : 0x7fffffff;
     for (int o = 32; o > 0; o >>= 1) imin = min(imin, __shfl_xor(imin, o));
-    if (active && i <= (int64_t)imin + a.drift) {
+    const bool part = active && i <= (int64_t)imin + a.drift;
+    // segments [jt, NS) hold no active slot of any lane taking part: the free tail
+    int kw = part ? klast : -1;
+    for (int o = 32; o > 0; o >>= 1) kw = max(kw, __shfl_xor(kw, o));
+    const int jt = __builtin_amdgcn_readfirstlane(kw < 0 ? 0 : kw / S + 1);
+    if (part) {
       ++n_lane_pass;
+      n_ws_slots += (unsigned)min(jt * S, N);
       double u0 = 0.0;
       bool changed = false;
+      int kl = -1;
       {
         Ric v{0, 0, 0, 0, 0, 0, 0, 0, 0};
-        SegIn<S> cur, nxt;
+        SegIn<S> cur;
         SegOut<S> g;
-        // sweep A: full backward Riccati, checkpoints at segment boundaries
-        if (PF) seg_load(a, a.NS - 1, L, i, fl, cur);
+        // sweep A, free tail: the s recursion, checkpoints of s
 #pragma unroll 1
-        for (int j = a.NS - 1; j >= 0; --j) {
-          if (!PF)
-            seg_load(a, j, L, i, fl, cur);
-          else if (j > 0)
-            seg_load(a, j - 1, L, i, fl, nxt);
-          ck_store(a, ck, j, v, lane);
+        for (int j = a.NS - 1; j >= jt; --j) {
+          seg_load<S, false>(a, j, L, i, fl, cur);
+          ck_store_s(ck, j, v, lane);
           if (j < jfull)
-            seg_riccati<S, true, false>(a, j, v, cur, g);
+            seg_tail<S, true, false>(a, tab, j, v, cur, g);
           else
-            seg_riccati<S, false, false>(a, j, v, cur, g);
-          if (PF) cur = nxt;
+            seg_tail<S, false, false>(a, tab, j, v, cur, g);
         }
-        // sweep B: per segment from the front — recompute its Riccati steps from the
-        // checkpoint, forward, then the costate back through it from λ at its end
-        double xs[3] = {x[0], a.T * x[1], a.Tsq * x[2]};  // ξ
-        Ric vn;
-        if (PF) {
-          seg_load(a, 0, L, i, fl, cur);
-          ck_load(ck, 0, v, lane);
+        if (jt < a.NS) {  // V at the tail's first slot: P from the table
+          const double* t = tab + (size_t)jt * S * TAB;
+          v.p00 = t[4];
+          v.p01 = t[5];
+          v.p02 = t[6];
+          v.p11 = t[7];
+          v.p12 = t[8];
+          v.p22 = t[9];
         }
+        // sweep A, working-set segments: full Riccati, checkpoints of (P, s)
 #pragma unroll 1
-        for (int j = 0; j < a.NS; ++j) {
-          if (!PF) {
-            seg_load(a, j, L, i, fl, cur);
-            ck_load(ck, j, v, lane);
-          } else if (j + 1 < a.NS) {
-            seg_load(a, j + 1, L, i, fl, nxt);
-            ck_load(ck, j + 1, vn, lane);
+        for (int j = jt - 1; j >= 0; --j) {
+          seg_load<S, true>(a, j, L, i, fl, cur);
+          ck_store(ck, j, v, lane);
+          const bool fr = seg_free(cur);
+          if (j < jfull) {
+            if (fr)
+              seg_riccati<S, true, false, true>(a, j, v, cur, g);
+            else
+              seg_riccati<S, true, false, false>(a, j, v, cur, g);
+          } else {
+            if (fr)
+              seg_riccati<S, false, false, true>(a, j, v, cur, g);
+            else
+              seg_riccati<S, false, false, false>(a, j, v, cur, g);
           }
-          const Ric ve = v;  // V at the segment's end
+        }
+        // sweep B: per segment from the front — recompute its steps from the checkpoint,
+        // forward, then (working-set segments) the costate back through it
+        double xs[3] = {x[0], a.T * x[1], a.Tsq * x[2]};  // ξ
+#pragma unroll 1
+        for (int j = 0; j < jt; ++j) {
+          seg_load<S, true>(a, j, L, i, fl, cur);
+          ck_load(ck, j, v, lane);
+          // (a free form here, as in sweep A, costs more registers than it saves)
           if (j < jfull)
-            seg_riccati<S, true, true>(a, j, v, cur, g);
+            seg_sweep_b<S, true>(a, j, v, cur, g, xs, u0, changed, kl, fl, lane);
           else
-            seg_riccati<S, false, true>(a, j, v, cur, g);
-          if (j < jfull)
-            seg_forward<S, true>(a, j, cur, g, xs, u0, changed, fl, lane);
-          else
-            seg_forward<S, false>(a, j, cur, g, xs, u0, changed, fl, lane);
-          double lam[3];
-          lam[0] = fma(ve.p00, xs[0], fma(ve.p01, xs[1], ve.p02 * xs[2])) - ve.s0;
-          lam[1] = fma(ve.p01, xs[0], fma(ve.p11, xs[1], ve.p12 * xs[2])) - ve.s1;
-          lam[2] = fma(ve.p02, xs[0], fma(ve.p12, xs[1], ve.p22 * xs[2])) - ve.s2;
-          if (j < jfull)
-            seg_costate<S, true>(a, j, cur, g, lam, changed, fl, lane);
-          else
-            seg_costate<S, false>(a, j, cur, g, lam, changed, fl, lane);
-          if (PF) {
-            cur = nxt;
-            v = vn;
+            seg_sweep_b<S, false>(a, j, v, cur, g, xs, u0, changed, kl, fl, lane);
+        }
+#pragma unroll 1
+        for (int j = jt; j < a.NS; ++j) {
+          seg_load<S, false>(a, j, L, i, fl, cur);
+          ck_load_s(ck, j, v, lane);
+          if (j < jfull) {
+            seg_tail<S, true, true>(a, tab, j, v, cur, g);
+            seg_forward_tail<S, true>(a, tab, j, cur, g, xs, u0, changed, kl, fl, lane);
+          } else {
+            seg_tail<S, false, true>(a, tab, j, v, cur, g);
+            seg_forward_tail<S, false>(a, tab, j, cur, g, xs, u0, changed, kl, fl, lane);
           }
         }
       }
@@ -449,9 +624,12 @@ __global__ void __launch_bounds__(64 * LQ_WAVES, W) zmpc_strict_lq_kernel(LqArgs
           // kept), this lane's column only
 #pragma unroll 8
           for (int k = 0; k < N - 1; ++k) fl[k * 64 + lane] = fl[(k + 1) * 64 + lane];
+          klast = (kl >= N - 1) ? N - 1 : max(kl - 1, -1);
         } else {
           active = false;
         }
+      } else {
+        klast = kl;
       }
     }
   }
@@ -461,10 +639,40 @@ __global__ void __launch_bounds__(64 * LQ_WAVES, W) zmpc_strict_lq_kernel(LqArgs
     else if (fq != 0)
       atomicOr(&a.status[b], fq);
   }
-  if (a.dbg) {
-    if (lane == 0) atomicAdd(a.dbg + 0, n_wave_pass);
-    for (int o = 32; o > 0; o >>= 1) n_lane_pass += __shfl_xor(n_lane_pass, o);
-    if (lane == 0) atomicAdd(a.dbg + 1, n_lane_pass);
+  if (a.cnt) {
+    for (int o = 32; o > 0; o >>= 1) {
+      n_lane_pass += __shfl_xor(n_lane_pass, o);
+      n_ws_slots += __shfl_xor(n_ws_slots, o);
+    }
+    if (lane == 0) {
+      atomicAdd(a.cnt + 0, n_wave_pass);
+      atomicAdd(a.cnt + 1, n_lane_pass);
+      atomicAdd(a.cnt + 2, n_ws_slots);
+      if (gw == 0) atomicAdd(a.cnt + 3, 1ull);
+    }
+  }
+}
+
+// The free-tail table of a plan: the Riccati recursion with every slot free, from V_N = 0
+// (ric_free, the arithmetic of the kernel's free steps; the bounds do not enter P, K, 1/Quu).
+__global__ void zmpc_strict_lq_table_kernel(LqArgs a, double* tab) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  Ric v{0, 0, 0, 0, 0, 0, 0, 0, 0};
+  for (int k = a.N - 1; k >= 0; --k) {
+    double K0, K1, K2, kf, iq;
+    ric_free(a, v, 0.0, K0, K1, K2, kf, iq);
+    double* t = tab + (size_t)k * TAB;
+    t[0] = K0;
+    t[1] = K1;
+    t[2] = K2;
+    t[3] = iq;
+    t[4] = v.p00;
+    t[5] = v.p01;
+    t[6] = v.p02;
+    t[7] = v.p11;
+    t[8] = v.p12;
+    t[9] = v.p22;
+    for (int c = 10; c < TAB; ++c) t[c] = 0.0;
   }
 }
 
@@ -517,30 +725,25 @@ hipError_t stage(const double* src, int64_t sb, int64_t st, int64_t sa, int64_t 
 // A/B only; default below).
 struct LqVariant {
   int S, W;
-  bool PF;  // next segment's loads prefetched
-  void (*kernel)(LqArgs);
+  void (*kernel)(LqArgs, const double*);
 };
 
 const LqVariant kLqVariants[] = {
-    {8, 2, false, zmpc_strict_lq_kernel<8, 2, false>},  // default
-    {8, 2, true, zmpc_strict_lq_kernel<8, 2, true>},
-    {8, 1, true, zmpc_strict_lq_kernel<8, 1, true>},
-    {4, 2, false, zmpc_strict_lq_kernel<4, 2, false>},
-    {4, 2, true, zmpc_strict_lq_kernel<4, 2, true>},
-    {4, 3, false, zmpc_strict_lq_kernel<4, 3, false>},
+    {8, 2, zmpc_strict_lq_kernel<8, 2>},  // default
+    {6, 2, zmpc_strict_lq_kernel<6, 2>},
+    {8, 1, zmpc_strict_lq_kernel<8, 1>},
 };
+constexpr int kMaxS = 8;
 
-// ZMPC_STRICT_LQ="SxW" or "SxWp" (prefetch) picks a variant for A/B runs.
 LqVariant lq_variant() {
   static LqVariant v = [] {
     LqVariant d = kLqVariants[0];
     const char* e = getenv("ZMPC_STRICT_LQ");
     if (e) {
       int s = 0, w = 0;
-      char pf = 0;
-      const int got = sscanf(e, "%dx%d%c", &s, &w, &pf);
-      for (const LqVariant& c : kLqVariants)
-        if (got >= 2 && c.S == s && c.W == w && c.PF == (got == 3 && pf == 'p')) d = c;
+      if (sscanf(e, "%dx%d", &s, &w) == 2)
+        for (const LqVariant& c : kLqVariants)
+          if (c.S == s && c.W == w) d = c;
     }
     return d;
   }();
@@ -571,27 +774,25 @@ void fill_consts(const zmpc_plan* p, LqArgs& a) {
     return e ? atoi(e) : 2;
   }();
   a.drift = drift;
+  a.cnt = p->lqcnt;
 }
 
-hipError_t launch_lq(LqArgs& a, int64_t waves, hipStream_t s) {
+hipError_t launch_lq(const zmpc_plan* p, LqArgs& a, int64_t waves, hipStream_t s) {
   static const bool dbg_on = getenv("ZMPC_DEBUG_STRICT") != nullptr;  // diagnostics only
-  static unsigned long long* dbgbuf = nullptr;
-  if (dbg_on && !dbgbuf) (void)hipMalloc((void**)&dbgbuf, 8 * sizeof(unsigned long long));
-  if (dbg_on && dbgbuf) {
-    (void)hipMemsetAsync(dbgbuf, 0, 8 * sizeof(unsigned long long), s);
-    a.dbg = dbgbuf;
-  }
   const LqVariant var = lq_variant();
   const int64_t blocks = (waves + LQ_WAVES - 1) / LQ_WAVES;
   const size_t lds = (size_t)LQ_WAVES * a.NS * var.S * 64;
-  hipLaunchKernelGGL(var.kernel, dim3((unsigned)blocks), dim3(64 * LQ_WAVES), lds, s, a);
+  hipLaunchKernelGGL(var.kernel, dim3((unsigned)blocks), dim3(64 * LQ_WAVES), lds, s, a,
+                     (const double*)p->lqtab);
   hipError_t e = hipGetLastError();
-  if (dbg_on && dbgbuf && e == hipSuccess) {
-    unsigned long long h[8];
+  if (dbg_on && a.cnt && e == hipSuccess) {
+    unsigned long long h[4];
     (void)hipStreamSynchronize(s);
-    (void)hipMemcpy(h, dbgbuf, sizeof(h), hipMemcpyDeviceToHost);
-    fprintf(stderr, "[zmpc strict-lq dbg] waves=%lld wave_passes=%llu lane_passes=%llu\n",
-            (long long)waves, h[0], h[1]);
+    (void)hipMemcpy(h, a.cnt, sizeof(h), hipMemcpyDeviceToHost);
+    fprintf(stderr,
+            "[zmpc strict-lq dbg] waves=%lld cumulative: launches=%llu wave_passes=%llu "
+            "lane_passes=%llu ws_slots=%llu\n",
+            (long long)waves, h[3], h[0], h[1], h[2]);
   }
   return e;
 }
@@ -608,8 +809,17 @@ hipError_t zmpc_strict_lq_set_attrs() {
 }
 
 bool zmpc_strict_lq_supported(const zmpc_plan* p) {
-  const size_t rows = (size_t)(p->N + 7) / 8 * 8;
-  return p->N >= 1 && (size_t)LQ_WAVES * rows * 64 <= 160 * 1024;
+  const size_t rows = (size_t)(p->N + kMaxS - 1) / kMaxS * kMaxS;
+  return p->N >= 1 && p->lqtab != nullptr && (size_t)LQ_WAVES * rows * 64 <= 160 * 1024;
+}
+
+size_t zmpc_strict_lq_table_doubles(int N) { return (size_t)N * TAB; }
+
+hipError_t zmpc_strict_lq_build_table(zmpc_plan* p, hipStream_t s) {
+  LqArgs a{};
+  fill_consts(p, a);
+  hipLaunchKernelGGL(zmpc_strict_lq_table_kernel, dim3(1), dim3(64), 0, s, a, p->lqtab);
+  return hipGetLastError();
 }
 
 hipError_t zmpc_launch_rollout_strict_lq(const zmpc_plan* p, int64_t B, int64_t n,
@@ -654,7 +864,7 @@ hipError_t zmpc_launch_rollout_strict_lq(const zmpc_plan* p, int64_t B, int64_t 
   if (e == hipSuccess) e = stage(zmin, bstride, 2, 1, n, Bst, a.rows, 2, tmin, s);
   a.zmax = tmax;
   a.zmin = tmin;
-  if (e == hipSuccess) e = launch_lq(a, waves, s);
+  if (e == hipSuccess) e = launch_lq(p, a, waves, s);
   hipError_t ef = hipFreeAsync(ws, s);
   return e != hipSuccess ? e : ef;
 }
@@ -694,7 +904,7 @@ hipError_t zmpc_launch_step_strict_lq(const zmpc_plan* p, int64_t B, const doubl
   if (e == hipSuccess) e = stage(zmin_win, p->N, 1, 0, p->N, B, a.rows, 1, tmin, s);
   a.zmax = tmax;
   a.zmin = tmin;
-  if (e == hipSuccess) e = launch_lq(a, waves, s);
+  if (e == hipSuccess) e = launch_lq(p, a, waves, s);
   hipError_t ef = hipFreeAsync(ws, s);
   return e != hipSuccess ? e : ef;
 }

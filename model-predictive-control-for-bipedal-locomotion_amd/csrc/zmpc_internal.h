@@ -44,6 +44,9 @@ struct zmpc_plan {
   // strict solver: persistent-grid slots and their per-wave factor scratch
   int strict_slots = 0;
   double* scratch = nullptr;  // [strict_slots * 4 * N * N]
+  // strict LQ solver (strict_lq.hip): free-tail Riccati table [N][16] and work counters
+  double* lqtab = nullptr;
+  unsigned long long* lqcnt = nullptr;  // [ZMPC_NCOUNTERS]
 };
 
 // kernels launchers (plan.hip)
@@ -89,6 +92,8 @@ hipError_t zmpc_launch_step_strict_lq(const zmpc_plan* p, int64_t B, const doubl
                                       std::string* why);
 bool zmpc_strict_lq_supported(const zmpc_plan* p);
 hipError_t zmpc_strict_lq_set_attrs();
+size_t zmpc_strict_lq_table_doubles(int N);
+hipError_t zmpc_strict_lq_build_table(zmpc_plan* p, hipStream_t s);
 
 hipError_t zmpc_rollout_unc_set_attrs();
 hipError_t zmpc_strict_set_attrs();

@@ -12,7 +12,8 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ZMPC_LIB", os.path.join(_HERE, "libzmpc.so"))
 
-ABI_VERSION = 2  # include/zmpc.h ZMPC_ABI_VERSION this binding is written for
+ABI_VERSION = 3  # include/zmpc.h ZMPC_ABI_VERSION this binding is written for
+NCOUNTERS = 4    # include/zmpc.h ZMPC_NCOUNTERS
 
 ZMPC_OK = 0
 ZMPC_EINVAL = -1
@@ -39,6 +40,8 @@ SIGNATURES = {
     "zmpc_plan_destroy": (ctypes.c_int, [ctypes.c_void_p]),
     "zmpc_plan_export": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32,
                                         ctypes.POINTER(ctypes.c_double), ctypes.c_int64]),
+    "zmpc_plan_counters": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
+                                          ctypes.c_int32, ctypes.c_int32]),
     "zmpc_step": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, _c_dbl_p, _c_dbl_p, _c_dbl_p,
                                  _c_dbl_p, ctypes.c_void_p, ctypes.c_void_p]),
     "zmpc_rollout": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, _c_dbl_p,

@@ -72,6 +72,15 @@ class Plan:
             return buf.reshape(self.N, self.N)
         return buf
 
+    def counters(self, reset: bool = False) -> dict:
+        """Strict solver work counters (zmpc_plan_counters, include/zmpc.h), summed over this
+        plan's launches since creation or the last reset; synchronises the device."""
+        buf = (ctypes.c_uint64 * _native.NCOUNTERS)()
+        rc = _native.load().zmpc_plan_counters(self._h, buf, _native.NCOUNTERS, int(reset))
+        _native.check(rc, "zmpc_plan_counters")
+        return {"wave_passes": int(buf[0]), "instance_passes": int(buf[1]),
+                "working_set_slots": int(buf[2]), "launches": int(buf[3])}
+
     # -- launches --------------------------------------------------------------------------
     def _dev(self):
         return torch.device("cuda", self.device)

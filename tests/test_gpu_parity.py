@@ -461,3 +461,22 @@ def test_strict_translation_invariance_full_batch():
     assert int(s1.abs().max()) == 0 and int(s2.abs().max()) == 0
     d = (h2 - h1).cpu().numpy()
     assert np.abs(d[..., 0] - 0.0625).max() <= 1e-7
+
+
+def test_strict_work_counters():
+    """zmpc_plan_counters: every solve takes at least one active-set pass; the working-set
+    slots are a part of all pass-slots; reset zeroes them."""
+    B = 128
+    zmax, zmin, x0, F, dt = synthetic_batch(B, 150, seed=11)
+    n = zmax.shape[1]
+    p = plan(150, strict=True, dt=dt)
+    p.counters(reset=True)
+    _, st = p.rollout(zmax, zmin, x0, kick=dt * F / M, kick_step=n // 2)
+    c = p.counters(reset=True)
+    assert int(st.abs().max()) == 0
+    assert c["launches"] == 1
+    solves = B * (n - 1) * 2
+    assert solves <= c["instance_passes"] <= 3 * solves
+    assert 0 < c["working_set_slots"] < c["instance_passes"] * 150
+    assert c["wave_passes"] * 64 >= c["instance_passes"]
+    assert p.counters()["launches"] == 0

@@ -92,7 +92,7 @@ def test_library_loads_and_exports_every_symbol():
     exported = set(re.findall(r" T (zmpc_\w+)", out))
     assert set(_header_symbols()) <= exported
     lib = _native.load()
-    assert lib.zmpc_abi_version() == _native.ABI_VERSION == 2
+    assert lib.zmpc_abi_version() == _native.ABI_VERSION == 3
     assert lib.zmpc_last_error() == b""
 
 
@@ -115,6 +115,9 @@ def test_argument_errors_without_gpu():
     assert rc == _native.ZMPC_EINVAL
     rc = lib.zmpc_cop_generate(0, 4, None, 0, None, None, None, None, None)
     assert rc == _native.ZMPC_EINVAL and b"params" in lib.zmpc_last_error()
+    buf = (ctypes.c_uint64 * _native.NCOUNTERS)()
+    rc = lib.zmpc_plan_counters(None, buf, _native.NCOUNTERS, 0)
+    assert rc == _native.ZMPC_EINVAL and b"NULL" in lib.zmpc_last_error()
 
 
 def test_router_errors():
