@@ -23,7 +23,7 @@
 //
 // Mapping: a lane owns one instance (one walk, one axis) for the whole rollout; a wave holds
 // 64 walks of one axis.  The bounds come in [axis][t][walk] (a staging transpose), so a wave's
-// load of one window slot is 512 contiguous bytes.  Per pass:
+// load of one window slot is 1 KiB contiguous ((z_max, z_min) pairs, 16 B per lane).  Per pass:
 //   sweep A  backward Riccati over the horizon in segments of S steps, checkpointing (P, s)
 //            at segment boundaries to a per-lane global slab (coalesced [.., 9, 64]);
 //   sweep B  per segment from the front: reload its checkpoint, recompute its S Riccati
@@ -62,14 +62,14 @@ struct LqArgs {
   int64_t n;             // samples per walk (rollout; 1 in window mode)
   int64_t nsteps;        // timesteps (n − 1, or 1)
   int64_t B;             // walks (rollout) or instances (step)
-  // staged bounds, tiled [axis][group of 64 walks][row][64]: row t of a window slot holds the
-  // group's 64 values for time t (rows past n − 1 repeat the last sample — the window padding
-  // of zmp_controller.py:81-88 — so no clamping in the kernel)
+  // staged bounds, tiled [axis][group of 64 walks][row][64] of (z_max, z_min) pairs: row t of a
+  // window slot holds the group's 64 pairs for time t, one 16-byte load per lane (rows past
+  // n − 1 repeat the last sample — the window padding of zmp_controller.py:81-88 — so no
+  // clamping in the kernel)
   int64_t rows;          // rows per (axis, group)
   int64_t groups;        // groups per axis in the staging (1 for a shared CoP)
   int shared;            // 1: every walk reads group 0 (bounds_stride = 0)
-  const double* zmax;
-  const double* zmin;
+  const double2* hl;
   const double* x0;      // rollout [B,2,3], step [B,3]
   const double* kick;    // [B] or null
   int64_t kick_step;
@@ -226,8 +226,7 @@ __device__ __forceinline__ void ric_tail(const LqArgs& a, Ric& v, double r, doub
 }
 
 struct Lane {
-  const double* hi;  // wave's staged z_max rows (uniform)
-  const double* lo;  // wave's staged z_min rows
+  const double2* hl;  // wave's staged (z_max, z_min) rows (uniform)
   int lane;
 };
 
@@ -236,16 +235,16 @@ struct Lane {
 template <int S, bool FLAGS>
 __device__ __forceinline__ void seg_load(const LqArgs& a, int j, const Lane& L, int64_t i,
                                          const unsigned char* fl, SegIn<S>& in) {
-  // segment's first row (the lane's own timestep); its S rows are 512 B apart: one address,
+  // segment's first row (the lane's own timestep); its S rows are 1 KiB apart: one address,
   // immediate offsets
   const int64_t row0 = i + a.toff + (int64_t)j * S;
-  const double* hp = L.hi + row0 * 64;
-  const double* lp = L.lo + row0 * 64;
+  const double2* hp = L.hl + row0 * 64;
   const unsigned char* fp = fl + j * S * 64;
 #pragma unroll
   for (int q = 0; q < S; ++q) {
-    in.hi[q] = hp[q * 64 + L.lane];
-    in.lo[q] = lp[q * 64 + L.lane];
+    const double2 v = hp[q * 64 + L.lane];
+    in.hi[q] = v.x;
+    in.lo[q] = v.y;
     if (FLAGS) in.f[q] = fp[q * 64 + L.lane];
   }
 }
@@ -479,8 +478,7 @@ __global__ void __launch_bounds__(64 * LQ_WAVES, W)
   {
     const int64_t g = a.shared ? 0 : (b0 >> 6);
     const int64_t off = ((int64_t)axis * a.groups + g) * a.rows * 64;
-    L.hi = a.zmax + off;
-    L.lo = a.zmin + off;
+    L.hl = a.hl + off;
   }
   const int jfull = N / S;  // segments [0, jfull) are full
   for (int k = 0; k < a.NS * S; ++k) fl[k * 64 + lane] = 0;
@@ -676,47 +674,52 @@ __global__ void zmpc_strict_lq_table_kernel(LqArgs a, double* tab) {
   }
 }
 
-// Stage bounds into the kernel's tiled layout: source element (b, t, axis) at
-// b·sb + min(t, nsrc − 1)·st + axis·sa → dst[((axis·G + b/64)·rows + t)·64 + b%64] for t < rows.
-// 64 walks × 32 rows per workgroup through LDS; consecutive threads read consecutive source
-// elements for the walk-contiguous [B, n, 2] layout and write consecutive destination ones.
+// Stage bounds into the kernel's tiled layout: source elements (b, t, axis) at
+// b·sb + min(t, nsrc − 1)·st + axis·sa of z_max and z_min → dst[((axis·G + b/64)·rows + t)·64
+// + b%64] = (z_max, z_min) for t < rows.  64 walks × 16 rows per workgroup through LDS;
+// consecutive threads read consecutive source elements for the walk-contiguous [B, n, 2]
+// layout and write consecutive destination pairs.
 struct StageArgs {
-  const double* src;
+  const double* hi;
+  const double* lo;
   int64_t sb, st, sa, nsrc;
   int64_t B, G, rows;
   int naxes;
-  double* dst;
+  double2* dst;
 };
 
 __global__ void __launch_bounds__(256) zmpc_bounds_stage_kernel(StageArgs s) {
-  __shared__ double tile[2][32][65];
-  const int64_t t0 = (int64_t)blockIdx.x * 32;
+  __shared__ double2 tile[2][16][65];
+  const int64_t t0 = (int64_t)blockIdx.x * 16;
   const int64_t b0 = (int64_t)blockIdx.y * 64;
-  const int per_walk = 32 * s.naxes;
+  const int per_walk = 16 * s.naxes;
   for (int idx = threadIdx.x; idx < 64 * per_walk; idx += 256) {
     const int w = idx / per_walk, rem = idx - w * per_walk;
     const int tt = rem / s.naxes, ax = rem - tt * s.naxes;
     const int64_t b = b0 + w;
     int64_t t = t0 + tt;
     if (t > s.nsrc - 1) t = s.nsrc - 1;  // window padding (zmp_controller.py:81-88)
-    double v = 0.0;
-    if (b < s.B) v = s.src[b * s.sb + t * s.st + ax * s.sa];
+    double2 v = make_double2(0.0, 0.0);
+    if (b < s.B) {
+      const int64_t e = b * s.sb + t * s.st + ax * s.sa;
+      v = make_double2(s.hi[e], s.lo[e]);
+    }
     tile[ax][tt][w] = v;
   }
   __syncthreads();
   for (int idx = threadIdx.x; idx < 64 * per_walk; idx += 256) {
     const int l = idx & 63, r = idx >> 6;
-    const int ax = r / 32, tt = r - ax * 32;
+    const int ax = r / 16, tt = r - ax * 16;
     const int64_t t = t0 + tt;
     if (t < s.rows)
       s.dst[((ax * s.G + (b0 >> 6)) * s.rows + t) * 64 + l] = tile[ax][tt][l];
   }
 }
 
-hipError_t stage(const double* src, int64_t sb, int64_t st, int64_t sa, int64_t nsrc, int64_t B,
-                 int64_t rows, int naxes, double* dst, hipStream_t s) {
-  StageArgs g{src, sb, st, sa, nsrc, B, (B + 63) / 64, rows, naxes, dst};
-  const dim3 grid((unsigned)((rows + 31) / 32), (unsigned)g.G);
+hipError_t stage(const double* hi, const double* lo, int64_t sb, int64_t st, int64_t sa,
+                 int64_t nsrc, int64_t B, int64_t rows, int naxes, double2* dst, hipStream_t s) {
+  StageArgs g{hi, lo, sb, st, sa, nsrc, B, (B + 63) / 64, rows, naxes, dst};
+  const dim3 grid((unsigned)((rows + 15) / 16), (unsigned)g.G);
   hipLaunchKernelGGL(zmpc_bounds_stage_kernel, grid, dim3(256), 0, s, g);
   return hipGetLastError();
 }
@@ -850,20 +853,17 @@ hipError_t zmpc_launch_rollout_strict_lq(const zmpc_plan* p, int64_t B, int64_t 
   a.groups = (Bst + 63) / 64;
   a.rows = n + (int64_t)a.NS * lq_variant().S;  // the last segment reads up to NS·S − 1 ahead
   const size_t ck_doubles = (size_t)waves * a.NS * 9 * 64;
-  const size_t st_doubles = (size_t)2 * a.groups * a.rows * 64;
+  const size_t st_doubles = (size_t)2 * a.groups * a.rows * 64 * 2;  // 2 axes, (hi, lo)
   double* ws = nullptr;
-  if ((e = hipMallocAsync((void**)&ws, (ck_doubles + 2 * st_doubles) * sizeof(double), s)) !=
+  if ((e = hipMallocAsync((void**)&ws, (ck_doubles + st_doubles) * sizeof(double), s)) !=
       hipSuccess) {
     *why = std::string("strict workspace allocation: ") + hipGetErrorString(e);
     return e;
   }
   a.ck = ws;
-  double* tmax = ws + ck_doubles;
-  double* tmin = tmax + st_doubles;
-  e = stage(zmax, bstride, 2, 1, n, Bst, a.rows, 2, tmax, s);
-  if (e == hipSuccess) e = stage(zmin, bstride, 2, 1, n, Bst, a.rows, 2, tmin, s);
-  a.zmax = tmax;
-  a.zmin = tmin;
+  double2* hl = reinterpret_cast<double2*>(ws + ck_doubles);
+  e = stage(zmax, zmin, bstride, 2, 1, n, Bst, a.rows, 2, hl, s);
+  a.hl = hl;
   if (e == hipSuccess) e = launch_lq(p, a, waves, s);
   hipError_t ef = hipFreeAsync(ws, s);
   return e != hipSuccess ? e : ef;
@@ -890,20 +890,17 @@ hipError_t zmpc_launch_step_strict_lq(const zmpc_plan* p, int64_t B, const doubl
   a.rows = (int64_t)a.NS * lq_variant().S;
   const int64_t waves = (B + 63) / 64;
   const size_t ck_doubles = (size_t)waves * a.NS * 9 * 64;
-  const size_t st_doubles = (size_t)a.groups * a.rows * 64;
+  const size_t st_doubles = (size_t)a.groups * a.rows * 64 * 2;  // (hi, lo)
   double* ws = nullptr;
-  hipError_t e = hipMallocAsync((void**)&ws, (ck_doubles + 2 * st_doubles) * sizeof(double), s);
+  hipError_t e = hipMallocAsync((void**)&ws, (ck_doubles + st_doubles) * sizeof(double), s);
   if (e != hipSuccess) {
     *why = std::string("strict workspace allocation: ") + hipGetErrorString(e);
     return e;
   }
   a.ck = ws;
-  double* tmax = ws + ck_doubles;
-  double* tmin = tmax + st_doubles;
-  e = stage(zmax_win, p->N, 1, 0, p->N, B, a.rows, 1, tmax, s);
-  if (e == hipSuccess) e = stage(zmin_win, p->N, 1, 0, p->N, B, a.rows, 1, tmin, s);
-  a.zmax = tmax;
-  a.zmin = tmin;
+  double2* hl = reinterpret_cast<double2*>(ws + ck_doubles);
+  e = stage(zmax_win, zmin_win, p->N, 1, 0, p->N, B, a.rows, 1, hl, s);
+  a.hl = hl;
   if (e == hipSuccess) e = launch_lq(p, a, waves, s);
   hipError_t ef = hipFreeAsync(ws, s);
   return e != hipSuccess ? e : ef;
