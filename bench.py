@@ -89,20 +89,66 @@ def walk_bounds(zmax_b, zmin_b, b):
     return zmax_b[b], zmin_b[b]
 
 
+def cpu_share():
+    """CPU cores this process may use: the affinity set, capped by the box's declared share
+    (OMP_NUM_THREADS is set to the GPU's CPU share on the GPU boxes) and at 16."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        n = min(n, int(os.environ.get("OMP_NUM_THREADS", n)))
+    except ValueError:
+        pass
+    return max(1, min(n, 16))
+
+
 def cpu_baseline(zmax_b, zmin_b, x0_b, kick_b, hist_gpu, cfg, budget_s):
-    """CPU path beside the GPU run (rank 0, N=1).  This leg is the only place bench.py touches
-    oracle/ — as the checker and the timed CPU baseline, never as the measured product.
+    """CPU path beside the GPU run (rank 0, N=1), SURVEY.md §8d.  This leg is the only place
+    bench.py touches oracle/ — as the checker and the timed CPU baseline, never as the measured
+    product.
       * value: the reference-faithful NumPy port (oracle predict_wieber_axis_ref: interpreted
         Px/Pu build + np.linalg.inv per solve, zmp_controller.py:162-199; strict: the exact
-        active-set box-QP restatement — the reference's cvxpy/OSQP is not installed), one BLAS
-        thread, whole walks of this batch until `budget_s` of CPU work is spent;
+        active-set box-QP restatement — the reference's cvxpy/OSQP is not installed) in P
+        processes x 1 BLAS thread (P = this process's CPU share), whole walks of this batch
+        until `budget_s` of CPU work per process; the sum of the processes' rates;
+      * single_process: the same port in this process, 1 BLAS thread;
       * optimized: the batched gain-form port (oracle rollout_gain, all BLAS threads) on the
         first walks (unconstrained configs);
       * parity: GPU vs port on those walks (CoM RMSE, max |Δstate|)."""
     from oracle import zmp_oracle as O
     from threadpoolctl import threadpool_limits
+    P = cpu_share()
+    first = 1 if len(x0_b) > 1 else 0
+    per = 6  # walks handed to each process (more than its budget needs)
+    jobs = []
+    for w in range(P):
+        idx = [first + w + P * m for m in range(per) if first + w + P * m < len(x0_b)]
+        if idx:
+            jobs.append((_walk_payload(zmax_b, zmin_b, x0_b, kick_b, hist_gpu, idx), cfg,
+                         budget_s))
+    multi = None
+    if jobs:
+        import multiprocessing
+        from concurrent.futures import ProcessPoolExecutor
+        # spawned children (the parent holds a GPU context: no fork); each runs numpy only
+        with ProcessPoolExecutor(max_workers=len(jobs),
+                                 mp_context=multiprocessing.get_context("spawn")) as ex:
+            res = list(ex.map(_port_worker, jobs))
+        solves = sum(r[0] for r in res)
+        multi = dict(value=sum(r[0] / r[1] for r in res if r[1] > 0), unit="QP solves/s",
+                     cores=len(jobs), kind="port",
+                     sample=f"{len(jobs)} processes x 1 BLAS thread, {solves} solves over "
+                            f"{sum(r[2] for r in res)} walk(s) of this batch, "
+                            f"{_port_what(cfg)}, ≈{budget_s:.0f} s of CPU work per process",
+                     com_rmse_gpu_vs_port=max(r[3] for r in res))
     with threadpool_limits(1):
-        out = _cpu_baseline(O, zmax_b, zmin_b, x0_b, kick_b, hist_gpu, cfg, budget_s)
+        single = _cpu_walks(O, _walk_payload(zmax_b, zmin_b, x0_b, kick_b, hist_gpu,
+                                             range(first, len(x0_b))), cfg, budget_s)
+    s_solves, s_el, s_walks, s_rms = single
+    single = dict(value=s_solves / s_el, unit="QP solves/s", cores=1, kind="port",
+                  sample=f"{s_walks} walk(s) = {s_solves} solves of this batch (walks "
+                         f"{first}..{first + s_walks - 1}), {_port_what(cfg)}, 1 BLAS thread",
+                  seconds=s_el, com_rmse_gpu_vs_port=s_rms)
+    out = dict(multi) if multi else dict(single)
+    out["single_process"] = single
     if not cfg.strict:
         nb = min(64, len(x0_b))
         zx = zmax_b if zmax_b.ndim == 3 else np.broadcast_to(zmax_b, (nb,) + zmax_b.shape)
@@ -113,7 +159,7 @@ def cpu_baseline(zmax_b, zmin_b, x0_b, kick_b, hist_gpu, cfg, budget_s):
                              cfg.Q, cfg.R, kick_b[:nb], n // 2)
         tg = time.perf_counter() - t0
         out["optimized"] = {"value": nb * (n - 1) * 2 / tg, "unit": "QP solves/s",
-                            "cores": os.cpu_count(), "kind": "port",
+                            "cores": P, "kind": "port",
                             "sample": f"first {nb} walks, batched gain-form NumPy port "
                                       "(oracle rollout_gain), default BLAS threads"}
         out["parity_first_walks"] = {
@@ -123,24 +169,46 @@ def cpu_baseline(zmax_b, zmin_b, x0_b, kick_b, hist_gpu, cfg, budget_s):
     return out
 
 
-def _cpu_baseline(O, zmax_b, zmin_b, x0_b, kick_b, hist_gpu, cfg, budget_s):
+def _port_what(cfg):
+    return ("exact active-set box-QP NumPy port (oracle rollout_strict; the reference's "
+            "cvxpy/OSQP is not installed)" if cfg.strict else
+            "reference-faithful NumPy port (interpreted Pu build + np.linalg.inv per solve, "
+            "zmp_controller.py:162-199)")
+
+
+def _walk_payload(zmax_b, zmin_b, x0_b, kick_b, hist_gpu, idx):
+    """(bounds, x0, kick, GPU CoM) of the walks idx, as plain arrays for a CPU worker."""
+    return [(*walk_bounds(zmax_b, zmin_b, b), x0_b[b], kick_b[b], hist_gpu[b, :, :, 0])
+            for b in idx]
+
+
+def _port_worker(job):
+    """One process of the multi-process CPU baseline (spawned; numpy only, 1 BLAS thread)."""
+    walks, cfg, budget_s = job
+    from oracle import zmp_oracle as O
+    from threadpoolctl import threadpool_limits
+    with threadpool_limits(1):
+        return _cpu_walks(O, walks, cfg, budget_s)
+
+
+def _cpu_walks(O, walks, cfg, budget_s):
+    """Time the CPU port over whole walks until budget_s; (solves, seconds, walks, max RMSE)."""
     N, dt = cfg.horizon, cfg.dt
-    solves, elapsed, walks, rms = 0, 0.0, 0, []
-    b = 1 if len(x0_b) > 1 else 0
-    first = b
-    while elapsed < budget_s and b < len(x0_b):
-        zmx, zmn = walk_bounds(zmax_b, zmin_b, b)
+    solves, elapsed, nw, rms = 0, 0.0, 0, []
+    for zmx, zmn, x0, kick, com_gpu in walks:
+        if elapsed >= budget_s:
+            break
         n = zmx.shape[0]
         t0 = time.perf_counter()
         if cfg.strict:
-            h = O.rollout_strict(x0_b[b, 0], x0_b[b, 1], zmx, zmn, N, dt, cfg.h, cfg.g, cfg.Q,
-                                 cfg.R, kick=kick_b[b], kick_step=n // 2)
+            h = O.rollout_strict(x0[0], x0[1], zmx, zmn, N, dt, cfg.h, cfg.g, cfg.Q,
+                                 cfg.R, kick=kick, kick_step=n // 2)
             com = h[:, :, 0]
         else:
             zx = np.vstack([zmx, np.tile(zmx[-1:], (N, 1))])
             zn = np.vstack([zmn, np.tile(zmn[-1:], (N, 1))])
-            x = x0_b[b, 0].reshape(3, 1).copy()
-            y = x0_b[b, 1].reshape(3, 1).copy()
+            x = x0[0].reshape(3, 1).copy()
+            y = x0[1].reshape(3, 1).copy()
             com = [[x[0, 0], y[0, 0]]]
             for i in range(n - 1):
                 if elapsed + time.perf_counter() - t0 > budget_s and i >= 16:
@@ -152,22 +220,14 @@ def _cpu_baseline(O, zmax_b, zmin_b, x0_b, kick_b, hist_gpu, cfg, budget_s):
                                               zn[i + 1:i + 1 + N, 1:2], dt, cfg.h, cfg.g,
                                               cfg.Q, cfg.R)
                 if i == n // 2:
-                    y = y - np.array([[0.0, kick_b[b], 0.0]]).T
+                    y = y - np.array([[0.0, kick, 0.0]]).T
                 com.append([x[0, 0], y[0, 0]])
             com = np.array(com)
         elapsed += time.perf_counter() - t0
         solves += 2 * (len(com) - 1)
-        rms.append(float(np.sqrt(np.mean((com - hist_gpu[b, :len(com), :, 0]) ** 2))))
-        walks += 1
-        b += 1
-    what = ("exact active-set box-QP NumPy port (oracle rollout_strict; the reference's "
-            "cvxpy/OSQP is not installed)" if cfg.strict else
-            "reference-faithful NumPy port (interpreted Pu build + np.linalg.inv per solve, "
-            "zmp_controller.py:162-199)")
-    return dict(value=solves / elapsed, unit="QP solves/s", cores=1, kind="port",
-                sample=f"{walks} walk(s) = {solves} solves of this batch (walks "
-                       f"{first}..{first + walks - 1}), {what}, 1 BLAS thread",
-                seconds=elapsed, com_rmse_gpu_vs_port=max(rms) if rms else None)
+        rms.append(float(np.sqrt(np.mean((com - com_gpu[:len(com)]) ** 2))))
+        nw += 1
+    return solves, elapsed, nw, (max(rms) if rms else None)
 
 
 def pmc_traffic(workload):
