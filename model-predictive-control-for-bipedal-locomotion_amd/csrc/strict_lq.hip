@@ -49,7 +49,7 @@
 
 namespace {
 
-constexpr int LQ_WAVES = 4;   // independent waves per workgroup
+constexpr int LQ_MAXWG = 8;   // most waves per workgroup of any variant (LDS sizing)
 constexpr int LQ_MAXIT = 64;  // active-set pass cap (as strict.hip)
 constexpr int TAB = 16;       // doubles per slot of the free-tail table: [0..2] K, [3] 1/Quu,
                               // [4..9] P after the slot (V_k: slots k..N−1 free), padding
@@ -452,12 +452,16 @@ __device__ __forceinline__ void ck_load_s(const double* ck, int j, Ric& v, int l
   v.s2 = p[512];
 }
 
-template <int S, int W>
-__global__ void __launch_bounds__(64 * LQ_WAVES, W)
+// G waves per workgroup.  G = 8: waves 0..3 take the x axis and 4..7 the y axis of the same
+// four 64-walk groups, so each SIMD (waves w and w + 4 under the round-robin placement) holds
+// one wave of each axis — the y axis carries nearly all of the active-set work, and an
+// axis-pure SIMD would idle once its x waves are done.  G = 4 (A/B): axis = wave parity.
+template <int S, int W, int G>
+__global__ void __launch_bounds__(64 * G, W)
     zmpc_strict_lq_kernel(LqArgs a, const double* __restrict__ tab) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lq_smem[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
-  const int64_t gw = (int64_t)blockIdx.x * LQ_WAVES + wave;
+  const int64_t gw = (int64_t)blockIdx.x * G + wave;
   const int N = a.N;
   // slot flags [NS·S][64] (rows past N stay 0: the last segment's loads are unguarded)
   unsigned char* fl = lq_smem + (size_t)wave * a.NS * S * 64;
@@ -467,6 +471,9 @@ __global__ void __launch_bounds__(64 * LQ_WAVES, W)
   if (a.window_mode) {
     axis = 0;
     b0 = gw * 64;
+  } else if (G == 8) {
+    axis = wave >> 2;
+    b0 = ((int64_t)blockIdx.x * 4 + (wave & 3)) * 64;
   } else {
     axis = (int)(gw & 1);
     b0 = (gw >> 1) * 64;
@@ -727,14 +734,15 @@ hipError_t stage(const double* hi, const double* lo, int64_t sb, int64_t st, int
 // Kernel variant: Riccati steps per segment S × waves per SIMD W (ZMPC_STRICT_LQ="SxW",
 // A/B only; default below).
 struct LqVariant {
-  int S, W;
+  int S, W, G;
   void (*kernel)(LqArgs, const double*);
 };
 
 const LqVariant kLqVariants[] = {
-    {8, 2, zmpc_strict_lq_kernel<8, 2>},  // default
-    {6, 2, zmpc_strict_lq_kernel<6, 2>},
-    {8, 1, zmpc_strict_lq_kernel<8, 1>},
+    {8, 2, 8, zmpc_strict_lq_kernel<8, 2, 8>},  // default
+    {8, 2, 4, zmpc_strict_lq_kernel<8, 2, 4>},
+    {6, 2, 8, zmpc_strict_lq_kernel<6, 2, 8>},
+    {8, 1, 8, zmpc_strict_lq_kernel<8, 1, 8>},
 };
 constexpr int kMaxS = 8;
 
@@ -743,10 +751,10 @@ LqVariant lq_variant() {
     LqVariant d = kLqVariants[0];
     const char* e = getenv("ZMPC_STRICT_LQ");
     if (e) {
-      int s = 0, w = 0;
-      if (sscanf(e, "%dx%d", &s, &w) == 2)
+      int s = 0, w = 0, g = 8;  // "SxW" or "SxWxG"
+      if (sscanf(e, "%dx%dx%d", &s, &w, &g) >= 2)
         for (const LqVariant& c : kLqVariants)
-          if (c.S == s && c.W == w) d = c;
+          if (c.S == s && c.W == w && c.G == g) d = c;
     }
     return d;
   }();
@@ -783,9 +791,9 @@ void fill_consts(const zmpc_plan* p, LqArgs& a) {
 hipError_t launch_lq(const zmpc_plan* p, LqArgs& a, int64_t waves, hipStream_t s) {
   static const bool dbg_on = getenv("ZMPC_DEBUG_STRICT") != nullptr;  // diagnostics only
   const LqVariant var = lq_variant();
-  const int64_t blocks = (waves + LQ_WAVES - 1) / LQ_WAVES;
-  const size_t lds = (size_t)LQ_WAVES * a.NS * var.S * 64;
-  hipLaunchKernelGGL(var.kernel, dim3((unsigned)blocks), dim3(64 * LQ_WAVES), lds, s, a,
+  const int64_t blocks = (waves + var.G - 1) / var.G;
+  const size_t lds = (size_t)var.G * a.NS * var.S * 64;
+  hipLaunchKernelGGL(var.kernel, dim3((unsigned)blocks), dim3(64 * var.G), lds, s, a,
                      (const double*)p->lqtab);
   hipError_t e = hipGetLastError();
   if (dbg_on && a.cnt && e == hipSuccess) {
@@ -813,7 +821,7 @@ hipError_t zmpc_strict_lq_set_attrs() {
 
 bool zmpc_strict_lq_supported(const zmpc_plan* p) {
   const size_t rows = (size_t)(p->N + kMaxS - 1) / kMaxS * kMaxS;
-  return p->N >= 1 && p->lqtab != nullptr && (size_t)LQ_WAVES * rows * 64 <= 160 * 1024;
+  return p->N >= 1 && p->lqtab != nullptr && (size_t)LQ_MAXWG * rows * 64 <= 160 * 1024;
 }
 
 size_t zmpc_strict_lq_table_doubles(int N) { return (size_t)N * TAB; }
@@ -852,7 +860,8 @@ hipError_t zmpc_launch_rollout_strict_lq(const zmpc_plan* p, int64_t B, int64_t 
   const int64_t Bst = a.shared ? 64 : B;  // a shared CoP is staged once, 64 identical lanes
   a.groups = (Bst + 63) / 64;
   a.rows = n + (int64_t)a.NS * lq_variant().S;  // the last segment reads up to NS·S − 1 ahead
-  const size_t ck_doubles = (size_t)waves * a.NS * 9 * 64;
+  const int64_t G = lq_variant().G;  // checkpoints for every wave of the launched blocks
+  const size_t ck_doubles = (size_t)((waves + G - 1) / G * G) * a.NS * 9 * 64;
   const size_t st_doubles = (size_t)2 * a.groups * a.rows * 64 * 2;  // 2 axes, (hi, lo)
   double* ws = nullptr;
   if ((e = hipMallocAsync((void**)&ws, (ck_doubles + st_doubles) * sizeof(double), s)) !=
@@ -889,7 +898,8 @@ hipError_t zmpc_launch_step_strict_lq(const zmpc_plan* p, int64_t B, const doubl
   a.groups = (B + 63) / 64;
   a.rows = (int64_t)a.NS * lq_variant().S;
   const int64_t waves = (B + 63) / 64;
-  const size_t ck_doubles = (size_t)waves * a.NS * 9 * 64;
+  const int64_t G = lq_variant().G;  // checkpoints for every wave of the launched blocks
+  const size_t ck_doubles = (size_t)((waves + G - 1) / G * G) * a.NS * 9 * 64;
   const size_t st_doubles = (size_t)a.groups * a.rows * 64 * 2;  // (hi, lo)
   double* ws = nullptr;
   hipError_t e = hipMallocAsync((void**)&ws, (ck_doubles + st_doubles) * sizeof(double), s);
