@@ -313,10 +313,12 @@ def main():
         launch()
     ev1.record(stream)
     torch.cuda.synchronize()
+    # this rank's time from the common start to its last launch finishing; the job time is
+    # the max over ranks (below), so the closing barrier's own latency is not charged
+    elapsed = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1) / args.steps
     work = plan.counters() if cfg.strict else None
     if world > 1:
