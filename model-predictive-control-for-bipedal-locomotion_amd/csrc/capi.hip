@@ -1,6 +1,7 @@
 // C-ABI of libzmpc.so (declared in include/zmpc.h).  Host-side only: argument checks,
 // device selection, buffer ownership of plans, error reporting.  No compute runs here.
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 
@@ -33,13 +34,22 @@ struct DeviceGuard {
   }
 };
 
+// A launcher's verdict: an argument it rejects comes with a reason (EINVAL), a failed
+// per-launch workspace allocation is hipErrorOutOfMemory (ENOMEM), anything else is HIP's.
+int launch_result(hipError_t e, const std::string& why, const char* what) {
+  if (e == hipSuccess) return ZMPC_OK;
+  if (!why.empty()) return fail(ZMPC_EINVAL, why);
+  if (e == hipErrorOutOfMemory)
+    return fail(ZMPC_ENOMEM, std::string(what) + ": device workspace allocation failed");
+  return hip_fail(e, (std::string(what) + " launch").c_str());
+}
+
 void free_plan(zmpc_plan* p) {
   if (!p) return;
   double* bufs[] = {p->p, p->Px, p->M, p->L, p->k, p->kx, p->X, p->G, p->v, p->Hz, p->scanP};
   for (double* b : bufs)
     if (b) (void)hipFree(b);
   if (p->info) (void)hipFree(p->info);
-  if (p->scratch) (void)hipFree(p->scratch);
   if (p->lqtab) (void)hipFree(p->lqtab);
   if (p->lqcnt) (void)hipFree(p->lqcnt);
   delete p;
@@ -64,6 +74,8 @@ int zmpc_plan_create(int device, int32_t N, double T, double T2_2, double T3_6, 
   if (N < 1 || N > 4096) return fail(ZMPC_EINVAL, "horizon N must be in [1, 4096]");
   if (!(T > 0) || !(Q > 0) || !(R >= 0))
     return fail(ZMPC_EINVAL, "need dt > 0, Q > 0, R >= 0");
+  if (strict && N > ZMPC_STRICT_MAX_N)
+    return fail(ZMPC_EINVAL, "strict horizon N must be <= " + std::to_string(ZMPC_STRICT_MAX_N));
   int ndev = 0;
   hipError_t e = hipGetDeviceCount(&ndev);
   if (e != hipSuccess) return hip_fail(e, "hipGetDeviceCount");
@@ -74,11 +86,13 @@ int zmpc_plan_create(int device, int32_t N, double T, double T2_2, double T3_6, 
     if ((e = zmpc_rollout_unc_set_attrs()) != hipSuccess) return hip_fail(e, "set LDS attrs");
     if ((e = zmpc_strict_set_attrs()) != hipSuccess) return hip_fail(e, "set LDS attrs");
     if ((e = zmpc_strict_lq_set_attrs()) != hipSuccess) return hip_fail(e, "set LDS attrs");
-    // the strict solver's per-launch workspace comes from the stream-ordered pool: keep
-    // freed blocks in the pool instead of returning them to the driver at every sync
+    // the strict solvers' per-launch workspaces come from the stream-ordered pool: keep up to
+    // ZMPC_POOL_KEEP_MB (default 4096) of freed blocks in the pool across synchronisations
+    // instead of returning them to the driver every time; anything above is released
     hipMemPool_t pool = nullptr;
     if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess && pool) {
-      uint64_t keep = ~0ull;
+      const char* env = getenv("ZMPC_POOL_KEEP_MB");
+      uint64_t keep = (uint64_t)(env ? atoll(env) : 4096) << 20;
       (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
     }
     attrs_done[device] = true;
@@ -124,11 +138,6 @@ int zmpc_plan_create(int device, int32_t N, double T, double T2_2, double T3_6, 
       return hip_fail(e, "hipDeviceGetAttribute");
     }
     P->strict_slots = 2 * cus;
-    const size_t bytes = (size_t)P->strict_slots * 4 * nn * sizeof(double);
-    if ((e = hipMalloc((void**)&P->scratch, bytes)) != hipSuccess) {
-      free_plan(P);
-      return fail(ZMPC_ENOMEM, std::string("hipMalloc scratch: ") + hipGetErrorString(e));
-    }
     if ((e = hipMalloc((void**)&P->lqtab, zmpc_strict_lq_table_doubles(N) * sizeof(double))) !=
             hipSuccess ||
         (e = hipMalloc((void**)&P->lqcnt, ZMPC_NCOUNTERS * sizeof(unsigned long long))) !=
@@ -240,9 +249,7 @@ int zmpc_step(const zmpc_plan* P, int64_t B, const double* x, const double* zmax
                                                      (hipStream_t)stream, &why)
                            : zmpc_launch_step_unc(P, B, x, zmax_win, zmin_win, x_next, status,
                                                   (hipStream_t)stream);
-  if (e != hipSuccess)
-    return why.empty() ? hip_fail(e, "zmpc_step launch") : fail(ZMPC_EINVAL, why);
-  return ZMPC_OK;
+  return launch_result(e, why, "zmpc_step");
 }
 
 static int rollout_impl(const zmpc_plan* P, int64_t B, int64_t n, const double* zmax,
@@ -268,9 +275,7 @@ static int rollout_impl(const zmpc_plan* P, int64_t B, int64_t n, const double* 
                            : zmpc_launch_rollout_unc(P, B, n, zmax, zmin, bounds_stride, x0,
                                                      kick, kick_step, kick_steps, hist, status,
                                                      s, &why);
-  if (e != hipSuccess)
-    return why.empty() ? hip_fail(e, "zmpc_rollout launch") : fail(ZMPC_EINVAL, why);
-  return ZMPC_OK;
+  return launch_result(e, why, "zmpc_rollout");
 }
 
 int zmpc_rollout(const zmpc_plan* P, int64_t B, int64_t n, const double* zmax,

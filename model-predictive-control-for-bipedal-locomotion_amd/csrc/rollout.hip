@@ -1031,70 +1031,198 @@ bool wide_geom(int N, int64_t n, WideGeom* g) {
   return (size_t)2 * g->lzp * sizeof(double) <= 64 * 1024;
 }
 
-// Longer walks (several correlation passes): one walk per wave, f through LDS.
+// Walks of any length (the fallback beyond the wide kernel's 64·8·8 + 1 samples): one wave per
+// walk, the walk processed in chunks of `lc` timesteps with the two axes' states carried in
+// registers from chunk to chunk, so the LDS footprint does not grow with n.  Per chunk: the
+// z_ref rows it reads (t0 .. t0 + lc + kc, clamped to the last sample — the window padding of
+// zmp_controller.py:81-88), the correlation passes into f (LDS), the lane-chunk affine scan
+// from the carried state, and the replay in the reference form through the dead z_ref area.
 template <int CW>
-__global__ void __launch_bounds__(64) zmpc_rollout_unc_long_kernel(RolloutArgs a) {
+__device__ __forceinline__ void chunk_scan_replay(const RolloutArgs& a, int lane, const double* f0,
+                                                  const double* f1, double* stage, int rows_pr,
+                                                  double* xs, double* ys, double kk,
+                                                  int64_t kstep, int64_t t0, int ns,
+                                                  double* hb) {
+  const LipmConsts lc = a.lc;
+  const double kx0 = a.kx[0], kx1 = a.kx[1], kx2 = a.kx[2];
+  const double Bv[3] = {lc.T3_6, lc.T2_2, lc.T};
+  Mat3 Ab;  // Ā = A − B kxᵀ
+  {
+    const double A[9] = {1.0, lc.T, lc.T2_2, 0.0, 1.0, lc.T, 0.0, 0.0, 1.0};
+    const double kx[3] = {kx0, kx1, kx2};
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) Ab.m[3 * i + j] = A[3 * i + j] - Bv[i] * kx[j];
+  }
+  const int C = (ns + 63) / 64;  // steps per lane chunk
+  const int mbeg = lane * C, mend = min(mbeg + C, ns);
+  // zero-start composition of the lane's steps, then Kogge-Stone with P = Ā^C
+  double s0[3] = {0.0, 0.0, 0.0}, s1[3] = {0.0, 0.0, 0.0};
+  for (int m = mbeg; m < mend; ++m) {
+    double t[3];
+    matvec3(Ab, s0, t);
+    for (int i = 0; i < 3; ++i) s0[i] = fma(Bv[i], f0[m], t[i]);
+    matvec3(Ab, s1, t);
+    for (int i = 0; i < 3; ++i) s1[i] = fma(Bv[i], f1[m], t[i]);
+    if (t0 + m == kstep) s1[1] -= kk;
+  }
+  Mat3 P = Ab;
+  for (int q = 1; q < C; ++q) P = matmul3(P, Ab);
+  if (lane == 0) {
+    double t[3];
+    matvec3(P, xs, t);
+    for (int i = 0; i < 3; ++i) s0[i] += t[i];
+    matvec3(P, ys, t);
+    for (int i = 0; i < 3; ++i) s1[i] += t[i];
+  }
+  Mat3 Pd = P;
+  for (int d = 1; d < 64; d <<= 1) {
+    double u0[3], u1[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      u0[i] = __shfl_up(s0[i], d, 64);
+      u1[i] = __shfl_up(s1[i], d, 64);
+    }
+    if (lane >= d) {
+      double t[3];
+      matvec3(Pd, u0, t);
+      for (int i = 0; i < 3; ++i) s0[i] += t[i];
+      matvec3(Pd, u1, t);
+      for (int i = 0; i < 3; ++i) s1[i] += t[i];
+    }
+    Pd = matmul3(Pd, Pd);
+  }
+  double xb0[3], yb0[3];  // state at the start of this lane's steps
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const double p0 = __shfl_up(s0[i], 1, 64);
+    const double p1 = __shfl_up(s1[i], 1, 64);
+    xb0[i] = (lane == 0) ? xs[i] : p0;
+    yb0[i] = (lane == 0) ? ys[i] : p1;
+  }
+  // replay x⁺ = A x + B u (zmp_controller.py:199) in rounds of staged rows t0+1 .. t0+ns
+  double x[3], y[3];
+  for (int r0 = 0; r0 < ns; r0 += rows_pr) {
+    const int r1 = min(r0 + rows_pr, ns);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      x[i] = xb0[i];
+      y[i] = yb0[i];
+    }
+    for (int m = mbeg; m < mend; ++m) {
+      const double ux = f0[m] - (kx0 * x[0] + kx1 * x[1] + kx2 * x[2]);
+      const double uy = f1[m] - (kx0 * y[0] + kx1 * y[1] + kx2 * y[2]);
+      double xn[3], yn[3];
+      lipm_step(lc, x, ux, xn);
+      lipm_step(lc, y, uy, yn);
+      if (t0 + m == kstep) yn[1] -= kk;  // F_ext impulse (:105-106)
+      if (m >= r0 && m < r1) {
+        double* o = stage + (m - r0) * 6;
+        o[0] = xn[0];
+        o[1] = xn[1];
+        o[2] = xn[2];
+        o[3] = yn[0];
+        o[4] = yn[1];
+        o[5] = yn[2];
+      }
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        x[i] = xn[i];
+        y[i] = yn[i];
+      }
+    }
+    __syncthreads();
+    const double2* src = reinterpret_cast<const double2*>(stage);
+    double2* dst = reinterpret_cast<double2*>(hb + (t0 + r0 + 1) * 6);
+    for (int e = lane; e < (r1 - r0) * 3; e += 64) dst[e] = src[e];
+    __syncthreads();
+  }
+  // carry the chunk's end state: the lane that ran step ns − 1
+  const int last = (ns - 1) / C;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    xs[i] = __shfl(x[i], last, 64);
+    ys[i] = __shfl(y[i], last, 64);
+  }
+}
+
+template <int CW>
+__global__ void __launch_bounds__(64) zmpc_rollout_unc_chunk_kernel(RolloutArgs a, int lc) {
   using ZL = ZrLayout<CW>;
   extern __shared__ __attribute__((aligned(16))) double smem[];
   const int64_t b = blockIdx.x;
   const int lane = threadIdx.x;
-  const int n = a.n, nsteps = n - 1;
-  const int passes = (nsteps + 64 * CW - 1) / (64 * CW);
+  const int n = a.n;
+  const int64_t nsteps = n - 1;
   double* ks = smem;
   double* zr0 = smem + a.kcp;
   double* zr1 = zr0 + a.lzp;
   double* f0 = zr1 + a.lzp;
-  double* f1 = f0 + ((nsteps + 2) & ~1);
+  double* f1 = f0 + lc;
+  const int rows_pr = (2 * a.lzp) / 6;  // history rows per staging round (z_ref area)
   for (int j = lane; j < a.kcp; j += 64) ks[j] = a.k[j];
-  {
-    const double2* zmx = reinterpret_cast<const double2*>(a.zmax + b * a.bstride);
-    const double2* zmn = reinterpret_cast<const double2*>(a.zmin + b * a.bstride);
-    constexpr int kU = 8;
-    for (int t0 = 0; t0 < n; t0 += 64 * kU) {
-      double2 hi[kU], lo[kU];
-#pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        const int t = t0 + u * 64 + lane;
-        if (t < n) {
-          hi[u] = zmx[t];
-          lo[u] = zmn[t];
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < kU; ++u) {
-        const int t = t0 + u * 64 + lane;
-        if (t < n) {
-          zr0[ZL::idx(t)] = (hi[u].x + lo[u].x) / 2;
-          zr1[ZL::idx(t)] = (hi[u].y + lo[u].y) / 2;
-        }
-      }
-    }
-    const double2 hi = zmx[n - 1], lo = zmn[n - 1];
-    const double last0 = (hi.x + lo.x) / 2, last1 = (hi.y + lo.y) / 2;
-    for (int t = n + lane; t < a.lz; t += 64) {
-      zr0[ZL::idx(t)] = last0;
-      zr1[ZL::idx(t)] = last1;
-    }
-  }
-  __syncthreads();
-  for (int pass = 0; pass < passes; ++pass) {
-    const int i0 = pass * 64 * CW + lane * CW;
-    double a0[CW], a1[CW];
-    correlate<CW>(a, ks, zr0, zr1, i0, a0, a1);
-#pragma unroll
-    for (int m = 0; m < CW; ++m) {
-      if (i0 + m < nsteps) {
-        f0[i0 + m] = a0[m];
-        f1[i0 + m] = a1[m];
-      }
-    }
-  }
-  __syncthreads();
+  const double2* zmx = reinterpret_cast<const double2*>(a.zmax + b * a.bstride);
+  const double2* zmn = reinterpret_cast<const double2*>(a.zmin + b * a.bstride);
   const double* xb = a.x0 + b * 6;
-  const double xi0[3] = {xb[0], xb[1], xb[2]};
-  const double xi1[3] = {xb[3], xb[4], xb[5]};
+  double xs[3] = {xb[0], xb[1], xb[2]}, ys[3] = {xb[3], xb[4], xb[5]};
   const double kk = (a.kick != nullptr) ? a.kick[b] : 0.0;
-  scan_replay_store<CW, false>(a, b, lane, nullptr, nullptr, f0, f1, zr0, xi0, xi1, kk);
+  const int64_t kstep = kick_step_of(a, b);
+  double* hb = a.hist + b * (int64_t)n * 6;
+  if (lane < 6) hb[lane] = xb[lane];  // row 0 = x0
+  for (int64_t t0 = 0; t0 < nsteps; t0 += lc) {
+    const int ns = (int)min((int64_t)lc, nsteps - t0);
+    const int passes = (ns + 64 * CW - 1) / (64 * CW);
+    const int lz = passes * 64 * CW + a.kc + 1;
+    __syncthreads();  // the previous chunk's staging rows are out
+    for (int t = lane; t < lz; t += 64) {
+      const int64_t row = min(t0 + t, (int64_t)n - 1);
+      const double2 h = zmx[row], l = zmn[row];
+      zr0[ZL::idx(t)] = (h.x + l.x) / 2;
+      zr1[ZL::idx(t)] = (h.y + l.y) / 2;
+    }
+    __syncthreads();
+    for (int pass = 0; pass < passes; ++pass) {
+      const int i0 = pass * 64 * CW + lane * CW;
+      double a0[CW], a1[CW];
+      correlate<CW>(a, ks, zr0, zr1, i0, a0, a1);
+#pragma unroll
+      for (int m = 0; m < CW; ++m) {
+        if (i0 + m < ns) {
+          f0[i0 + m] = a0[m];
+          f1[i0 + m] = a1[m];
+        }
+      }
+    }
+    __syncthreads();  // f complete; the z_ref area becomes the history staging
+    chunk_scan_replay<CW>(a, lane, f0, f1, zr0, rows_pr, xs, ys, kk, kstep, t0, ns, hb);
+  }
+  if (a.status != nullptr) {
+    const bool finite = isfinite(xs[0]) && isfinite(xs[1]) && isfinite(xs[2]) &&
+                        isfinite(ys[0]) && isfinite(ys[1]) && isfinite(ys[2]);
+    if (lane == 0) a.status[b] = finite ? 0 : ZMPC_ST_NONFINITE;
+  }
+}
+
+// Chunk geometry: CW = 8, chunks of lc = 2·64·CW timesteps (two correlation passes), LDS =
+// k + z_ref (2 axes, lc + kc + 1 padded rows) + f (2 axes × lc): ≈ 45 KB at N = 512.
+struct ChunkGeom {
+  int lc, kc, kcp, lz, lzp;
+};
+
+ChunkGeom chunk_geom(int N) {
+  constexpr int CW = 8;
+  ChunkGeom g;
+  g.lc = 2 * 64 * CW;
+  g.kc = (N + CW - 1) / CW * CW;
+  g.kcp = (g.kc + CW + 1) & ~1;  // the correlation's sliding window reads one group past kc
+  g.lz = g.lc + g.kc + 1;
+  g.lzp = ((g.lz + g.lz / CW + 1) + 1) & ~1;
+  return g;
+}
+
+size_t chunk_lds_bytes(const ChunkGeom& g) {
+  return (size_t)(g.kcp + 2 * g.lzp + 2 * g.lc) * sizeof(double);
 }
 
 // Batched predict_wieber_axis (strict=False): one wave per instance.
@@ -1126,6 +1254,18 @@ __global__ void __launch_bounds__(256) zmpc_step_unc_kernel(
 }
 
 int g_cus = 0;  // CUs of the device the attributes were set on (grid sizing)
+
+// Any walk length: the chunked kernel (its own CW = 8 geometry).
+void launch_chunk(hipStream_t s, const RolloutArgs& a0, int N) {
+  const ChunkGeom g = chunk_geom(N);
+  RolloutArgs a = a0;
+  a.kc = g.kc;
+  a.kcp = g.kcp;
+  a.lz = g.lz;
+  a.lzp = g.lzp;
+  hipLaunchKernelGGL(zmpc_rollout_unc_chunk_kernel<8>, dim3((unsigned)a.B), dim3(64),
+                     chunk_lds_bytes(g), s, a, g.lc);
+}
 
 template <int CW>
 void launch_unc(const RolloutGeom& g, size_t lds, hipStream_t s, const RolloutArgs& a) {
@@ -1161,11 +1301,8 @@ void launch_unc(const RolloutGeom& g, size_t lds, hipStream_t s, const RolloutAr
     b.srows = (int)(lds_axis / (6 * sizeof(double)));
     hipLaunchKernelGGL(zmpc_rollout_unc_axis_kernel<CW>, dim3((unsigned)a.B), dim3(128), lds_axis,
                        s, b);
-  } else if (g.passes == 1) {
-    hipLaunchKernelGGL(zmpc_rollout_unc_kernel<CW>, dim3((unsigned)a.B), dim3(64), lds, s, a);
   } else {
-    hipLaunchKernelGGL(zmpc_rollout_unc_long_kernel<CW>, dim3((unsigned)a.B), dim3(64), lds, s,
-                       a);
+    hipLaunchKernelGGL(zmpc_rollout_unc_kernel<CW>, dim3((unsigned)a.B), dim3(64), lds, s, a);
   }
 }
 
@@ -1188,10 +1325,6 @@ hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, con
   }
   const RolloutGeom g = rollout_geom(p->N, n);
   const size_t lds = lds_bytes(g);
-  if (lds > 160 * 1024) {
-    *why = "walk too long for the LDS-resident rollout (n=" + std::to_string(n) + ")";
-    return hipErrorInvalidValue;
-  }
   static const int dbg = [] {
     const char* e = getenv("ZMPC_DEBUG_ROLLOUT");  // diagnostic ablation bits (0 in production)
     return e ? atoi(e) : 0;
@@ -1200,8 +1333,16 @@ hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, con
                 p->k, p->kx,  zmax,      zmin,  bstride,    x0,  kick,
                 kick_step,    hist, status, p->scanP, dbg, 0, kick_steps};
   WideGeom wg;
-  static const bool no_wide = getenv("ZMPC_ROLLOUT_NO_WIDE") != nullptr;  // A/B: long kernel
-  if (!no_wide && g.passes > 1 && wide_geom(p->N, n, &wg)) {
+  static const bool no_wide = getenv("ZMPC_ROLLOUT_NO_WIDE") != nullptr;  // A/B: chunk kernel
+  if (g.passes > 1 && (no_wide || !wide_geom(p->N, n, &wg))) {
+    launch_chunk(s, a, p->N);  // any length (the whole walk does not fit one pass)
+    return hipGetLastError();
+  }
+  if (lds > 160 * 1024) {  // single-pass geometry beyond LDS (very long horizon N)
+    launch_chunk(s, a, p->N);
+    return hipGetLastError();
+  }
+  if (g.passes > 1) {
     RolloutArgs q = a;
     q.kc = wg.kc;
     q.lz = wg.lz;
@@ -1253,12 +1394,12 @@ hipError_t zmpc_rollout_unc_set_attrs() {
 #define ZMPC_ATTR(C)                                                                        \
   if (e == hipSuccess)                                                                      \
     e = hipFuncSetAttribute((const void*)zmpc_rollout_unc_kernel<C>,                       \
-                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);       \
-  if (e == hipSuccess)                                                                      \
-    e = hipFuncSetAttribute((const void*)zmpc_rollout_unc_long_kernel<C>,                  \
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   ZMPC_ATTR(1) ZMPC_ATTR(2) ZMPC_ATTR(3) ZMPC_ATTR(4) ZMPC_ATTR(5) ZMPC_ATTR(6) ZMPC_ATTR(7)
   ZMPC_ATTR(8)
 #undef ZMPC_ATTR
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)zmpc_rollout_unc_chunk_kernel<8>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
   return e;
 }

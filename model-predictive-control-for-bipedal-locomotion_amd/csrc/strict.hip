@@ -55,7 +55,8 @@ struct StrictArgs {
   const int64_t* kick_steps;  // [B] per-walk kick steps, or null
   double* out;           // rollout hist [B,n,2,3], step x_next [B,3]
   int32_t* status;       // [B] or null
-  double* scratch;       // per-wave N*N factor scratch (gridDim*SWAVES slots)
+  double* scratch;       // per-wave factor scratch, sg_stride doubles each (gridDim*SWAVES slots)
+  int64_t sg_stride;     // (N/2 + 1)²: the reduced system is min(|A|, |F|) <= N/2
   unsigned long long* dbg;  // diagnostic phase counters (ZMPC_DEBUG_STRICT), null normally
   int lds_chol;          // A/B: 1 = LDS Cholesky for every reduced size (ZMPC_STRICT_LDS_CHOL)
   int gsz;               // doubles of LDS holding G packed (0: G read from L2)
@@ -676,7 +677,7 @@ __global__ void __launch_bounds__(256) zmpc_strict_kernel(StrictArgs a) {
   w.ia = reinterpret_cast<int*>(my + 4 * Np);
   w.iff = w.ia + Np;
   w.S = my + 5 * Np;
-  w.Sg = a.scratch + ((size_t)blockIdx.x * SWAVES + wave) * (size_t)a.N * a.N;
+  w.Sg = a.scratch + ((size_t)blockIdx.x * SWAVES + wave) * (size_t)a.sg_stride;
   w.Gs = nullptr;
   if (a.gsz > 0) {
     // G (symmetric, batch-invariant) packed into LDS once per workgroup: every reduced-matrix
@@ -852,7 +853,16 @@ static hipError_t launch_strict(const zmpc_plan* p, StrictArgs a, hipStream_t s,
   a.p0 = p->T3_6 - p->Thg;
   const int64_t ntiles = (a.ninst + SNB - 1) / SNB;
   int grid = (int)std::min<int64_t>(ntiles, (int64_t)p->strict_slots);
-  a.scratch = p->scratch;
+  // the global factor room of the waves (reduced systems that fit neither registers nor the
+  // packed LDS factor) is allocated per launch, stream-ordered, so concurrent launches of one
+  // plan on different streams never share it; m = min(|A|, |F|) <= N/2 bounds its size
+  const int64_t half1 = p->N / 2 + 1;
+  a.sg_stride = half1 * half1;
+  const size_t sg_bytes = (size_t)grid * SWAVES * (size_t)a.sg_stride * sizeof(double);
+  if (hipMallocAsync((void**)&a.scratch, sg_bytes, s) != hipSuccess) {
+    (void)hipGetLastError();
+    return hipErrorOutOfMemory;
+  }
   const size_t lds = strict_lds_bytes(a.Np, a.ld, a.pcap, a.gsz);
   static const bool lds_chol = getenv("ZMPC_STRICT_LDS_CHOL") != nullptr;  // A/B only
   a.lds_chol = lds_chol ? 1 : 0;
@@ -873,10 +883,13 @@ static hipError_t launch_strict(const zmpc_plan* p, StrictArgs a, hipStream_t s,
     ZMPC_SCASE(7) ZMPC_SCASE(8)
 #undef ZMPC_SCASE
     default:
+      (void)hipFreeAsync(a.scratch, s);
       *why = "unsupported horizon";
       return hipErrorInvalidValue;
   }
   hipError_t e = hipGetLastError();
+  const hipError_t ef = hipFreeAsync(a.scratch, s);
+  if (e == hipSuccess) e = ef;
   if (dbg_on && dbgbuf && e == hipSuccess) {
     unsigned long long h[32];
     (void)hipStreamSynchronize(s);

@@ -49,7 +49,6 @@
 
 namespace {
 
-constexpr int LQ_MAXWG = 8;   // most waves per workgroup of any variant (LDS sizing)
 constexpr int LQ_MAXIT = 64;  // active-set pass cap (as strict.hip)
 constexpr int TAB = 16;       // doubles per slot of the free-tail table: [0..2] K, [3] 1/Quu,
                               // [4..9] P after the slot (V_k: slots k..N−1 free), padding
@@ -740,11 +739,13 @@ struct LqVariant {
 
 const LqVariant kLqVariants[] = {
     {8, 2, 8, zmpc_strict_lq_kernel<8, 2, 8>},  // default
-    {8, 2, 4, zmpc_strict_lq_kernel<8, 2, 4>},
+    {8, 2, 4, zmpc_strict_lq_kernel<8, 2, 4>},  // N up to 640 (slot flags of 4 waves in LDS)
+    {8, 2, 2, zmpc_strict_lq_kernel<8, 2, 2>},  // N up to 1280
+    {8, 2, 1, zmpc_strict_lq_kernel<8, 2, 1>},  // N up to 2560
     {6, 2, 8, zmpc_strict_lq_kernel<6, 2, 8>},
     {8, 1, 8, zmpc_strict_lq_kernel<8, 1, 8>},
 };
-constexpr int kMaxS = 8;
+constexpr size_t kLdsCap = 160 * 1024;
 
 LqVariant lq_variant() {
   static LqVariant v = [] {
@@ -759,6 +760,18 @@ LqVariant lq_variant() {
     return d;
   }();
   return v;
+}
+
+// The configured variant, or — when its G waves' slot flags (G × ⌈N/S⌉·S × 64 bytes) do not
+// fit a CU's LDS — the same S and W with the largest G that fits (N ≤ 2560 at G = 1).
+LqVariant lq_variant_for(int N) {
+  const LqVariant v = lq_variant();
+  const size_t rows = (size_t)(N + v.S - 1) / v.S * v.S;
+  if ((size_t)v.G * rows * 64 <= kLdsCap) return v;
+  for (int g = v.G / 2; g >= 1; g /= 2)
+    for (const LqVariant& c : kLqVariants)
+      if (c.S == v.S && c.W == v.W && c.G == g && (size_t)g * rows * 64 <= kLdsCap) return c;
+  return LqVariant{v.S, v.W, 0, nullptr};
 }
 
 void fill_consts(const zmpc_plan* p, LqArgs& a) {
@@ -790,7 +803,7 @@ void fill_consts(const zmpc_plan* p, LqArgs& a) {
 
 hipError_t launch_lq(const zmpc_plan* p, LqArgs& a, int64_t waves, hipStream_t s) {
   static const bool dbg_on = getenv("ZMPC_DEBUG_STRICT") != nullptr;  // diagnostics only
-  const LqVariant var = lq_variant();
+  const LqVariant var = lq_variant_for(p->N);
   const int64_t blocks = (waves + var.G - 1) / var.G;
   const size_t lds = (size_t)var.G * a.NS * var.S * 64;
   hipLaunchKernelGGL(var.kernel, dim3((unsigned)blocks), dim3(64 * var.G), lds, s, a,
@@ -820,8 +833,8 @@ hipError_t zmpc_strict_lq_set_attrs() {
 }
 
 bool zmpc_strict_lq_supported(const zmpc_plan* p) {
-  const size_t rows = (size_t)(p->N + kMaxS - 1) / kMaxS * kMaxS;
-  return p->N >= 1 && p->lqtab != nullptr && (size_t)LQ_MAXWG * rows * 64 <= 160 * 1024;
+  return p->N >= 1 && p->N <= ZMPC_STRICT_MAX_N && p->lqtab != nullptr &&
+         lq_variant_for(p->N).kernel != nullptr;
 }
 
 size_t zmpc_strict_lq_table_doubles(int N) { return (size_t)N * TAB; }
@@ -860,14 +873,13 @@ hipError_t zmpc_launch_rollout_strict_lq(const zmpc_plan* p, int64_t B, int64_t 
   const int64_t Bst = a.shared ? 64 : B;  // a shared CoP is staged once, 64 identical lanes
   a.groups = (Bst + 63) / 64;
   a.rows = n + (int64_t)a.NS * lq_variant().S;  // the last segment reads up to NS·S − 1 ahead
-  const int64_t G = lq_variant().G;  // checkpoints for every wave of the launched blocks
+  const int64_t G = lq_variant_for(p->N).G;  // checkpoints for every wave of the launched blocks
   const size_t ck_doubles = (size_t)((waves + G - 1) / G * G) * a.NS * 9 * 64;
   const size_t st_doubles = (size_t)2 * a.groups * a.rows * 64 * 2;  // 2 axes, (hi, lo)
   double* ws = nullptr;
-  if ((e = hipMallocAsync((void**)&ws, (ck_doubles + st_doubles) * sizeof(double), s)) !=
-      hipSuccess) {
-    *why = std::string("strict workspace allocation: ") + hipGetErrorString(e);
-    return e;
+  if (hipMallocAsync((void**)&ws, (ck_doubles + st_doubles) * sizeof(double), s) != hipSuccess) {
+    (void)hipGetLastError();
+    return hipErrorOutOfMemory;  // ZMPC_ENOMEM at the C-ABI
   }
   a.ck = ws;
   double2* hl = reinterpret_cast<double2*>(ws + ck_doubles);
@@ -898,15 +910,15 @@ hipError_t zmpc_launch_step_strict_lq(const zmpc_plan* p, int64_t B, const doubl
   a.groups = (B + 63) / 64;
   a.rows = (int64_t)a.NS * lq_variant().S;
   const int64_t waves = (B + 63) / 64;
-  const int64_t G = lq_variant().G;  // checkpoints for every wave of the launched blocks
+  const int64_t G = lq_variant_for(p->N).G;  // checkpoints for every wave of the launched blocks
   const size_t ck_doubles = (size_t)((waves + G - 1) / G * G) * a.NS * 9 * 64;
   const size_t st_doubles = (size_t)a.groups * a.rows * 64 * 2;  // (hi, lo)
   double* ws = nullptr;
-  hipError_t e = hipMallocAsync((void**)&ws, (ck_doubles + st_doubles) * sizeof(double), s);
-  if (e != hipSuccess) {
-    *why = std::string("strict workspace allocation: ") + hipGetErrorString(e);
-    return e;
+  if (hipMallocAsync((void**)&ws, (ck_doubles + st_doubles) * sizeof(double), s) != hipSuccess) {
+    (void)hipGetLastError();
+    return hipErrorOutOfMemory;  // ZMPC_ENOMEM at the C-ABI
   }
+  hipError_t e = hipSuccess;
   a.ck = ws;
   double2* hl = reinterpret_cast<double2*>(ws + ck_doubles);
   e = stage(zmax_win, zmin_win, p->N, 1, 0, p->N, B, a.rows, 1, hl, s);

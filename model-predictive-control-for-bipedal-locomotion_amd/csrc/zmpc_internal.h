@@ -15,6 +15,10 @@
 constexpr int kScanLevels = 7;
 constexpr int kScanStride = kScanLevels * 9;
 
+// Longest strict horizon: the LQ kernel's per-wave slot flags ([N][64] bytes) must fit a CU's
+// LDS for one wave per workgroup (strict_lq.hip lq_variant_for).
+constexpr int ZMPC_STRICT_MAX_N = 2560;
+
 struct LipmConsts {
   double T;     // A[0,1] = A[1,2] = B[2]
   double T2_2;  // A[0,2] = B[1]
@@ -41,9 +45,9 @@ struct zmpc_plan {
   double* v = nullptr;   // [N]   first column of Pu⁻¹ (strict plans)
   double* Hz = nullptr;  // [N,N] Q I + R Pu⁻ᵀPu⁻¹ = G⁻¹ (strict plans)
   int* info = nullptr;   // [1] factorisation status
-  // strict solver: persistent-grid slots and their per-wave factor scratch
+  // strict reduced-Cholesky solver (strict.hip): persistent-grid slots (its factor scratch is
+  // allocated per launch, stream-ordered)
   int strict_slots = 0;
-  double* scratch = nullptr;  // [strict_slots * 4 * N * N]
   // strict LQ solver (strict_lq.hip): free-tail Riccati table [N][16] and work counters
   double* lqtab = nullptr;
   unsigned long long* lqcnt = nullptr;  // [ZMPC_NCOUNTERS]

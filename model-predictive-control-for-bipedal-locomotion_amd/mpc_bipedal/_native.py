@@ -64,6 +64,10 @@ class NativeError(RuntimeError):
     """A libzmpc call failed (message from zmpc_last_error)."""
 
 
+class DeviceOutOfMemory(NativeError, MemoryError):
+    """ZMPC_ENOMEM: a plan or per-launch workspace allocation on the device failed."""
+
+
 def load():
     """Load libzmpc.so once; raise with a build hint if it is not there."""
     global _lib
@@ -90,4 +94,6 @@ def check(rc: int, what: str):
         msg = load().zmpc_last_error().decode(errors="replace")
         if rc == ZMPC_EINVAL:
             raise ValueError(f"{what}: {msg}")
+        if rc == ZMPC_ENOMEM:
+            raise DeviceOutOfMemory(f"{what} failed ({rc}): {msg}")
         raise NativeError(f"{what} failed ({rc}): {msg}")

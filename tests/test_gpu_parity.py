@@ -274,10 +274,11 @@ def test_shared_cop_equals_dense():
     assert torch.equal(h_shared, h_dense)
 
 
-@pytest.mark.parametrize("n", (1, 2, 3, 65, 130, 513, 514, 700, 1100, 2500, 4097))
+@pytest.mark.parametrize("n", (1, 2, 3, 65, 130, 513, 514, 700, 1100, 2500, 4097, 4098, 6000))
 def test_walk_lengths(n):
     """Ragged lengths: n=1 (no solve), chunk boundaries of the lane scan, the single-pass /
-    wide (2, 4, 8 waves per axis) kernel boundaries (513 | 514, 1025, 2049, 4097)."""
+    wide (2, 4, 8 waves per axis) kernel boundaries (513 | 514, 1025, 2049, 4097) and the
+    chunked kernel beyond (4098: one full 1024-step chunk plus a partial one, 6000)."""
     rng = np.random.default_rng(n)
     N = 40
     dt = 1.5 / N
@@ -289,6 +290,59 @@ def test_walk_lengths(n):
     hist, _ = p.rollout(zmax, zmin, x0, kick=kick, kick_step=n // 2)
     ref = O.rollout_gain(zmax, zmin, x0, N, dt, H, G, Q, R, kick, n // 2)
     assert np.abs(hist.cpu().numpy() - ref).max() <= 1e-8
+
+
+@pytest.mark.parametrize("N,n", ((512, 3649), (512, 3650), (512, 5000), (150, 6001)))
+def test_long_walks_any_length(N, n):
+    """Walks longer than one LDS-resident pass (n > 3649 at N = 512 was rejected before the
+    chunked kernel): every walk vs the oracle, kick in the second chunk."""
+    rng = np.random.default_rng(N + n)
+    dt = 1.5 / N
+    ctr = np.cumsum(rng.normal(0, 0.004, (2, n, 2)), 1)
+    zmax, zmin = ctr + 0.05, ctr - 0.05
+    x0 = rng.normal(0, 0.01, (2, 2, 3))
+    kick = np.array([0.05, -0.1])
+    p = plan(N, dt=dt)
+    hist, st = p.rollout(zmax, zmin, x0, kick=kick, kick_step=1500)
+    assert int(st.abs().max()) == 0
+    ref = O.rollout_gain(zmax, zmin, x0, N, dt, H, G, Q, R, kick, 1500)
+    assert np.abs(hist.cpu().numpy() - ref).max() <= 1e-8
+
+
+_CHUNK_CHILD = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, sys.argv[1])
+from mpc_bipedal.solver import Plan
+d = np.load(sys.argv[2])
+p = Plan(0, int(d["N"]), float(d["dt"]), 0.75, 9.81, 1.0, 1e-6, False)
+h, _ = p.rollout(d["zmax"], d["zmin"], d["x0"], kick=d["kick"], kick_step=int(d["ks"]))
+np.save(sys.argv[3], h.cpu().numpy())
+"""
+
+
+def test_chunk_kernel_equals_wide_kernel(tmp_path):
+    """The chunked kernel (forced with ZMPC_ROLLOUT_NO_WIDE) and the wide kernel agree on
+    walks the wide kernel covers (514 <= n <= 4097)."""
+    import subprocess
+    import sys
+    rng = np.random.default_rng(9)
+    outs = []
+    for n in (700, 3000):
+        ctr = np.cumsum(rng.normal(0, 0.004, (5, n, 2)), 1)
+        inp = tmp_path / f"in{n}.npz"
+        np.savez(inp, N=150, dt=0.01, zmax=ctr + 0.05, zmin=ctr - 0.05,
+                 x0=rng.normal(0, 0.01, (5, 2, 3)), kick=rng.uniform(0, 0.1, 5), ks=n // 2)
+        res = []
+        for no_wide in (False, True):
+            out = tmp_path / f"h{n}{int(no_wide)}.npy"
+            env = dict(os.environ)
+            if no_wide:
+                env["ZMPC_ROLLOUT_NO_WIDE"] = "1"
+            subprocess.run([sys.executable, "-c", _CHUNK_CHILD, PKG, str(inp), str(out)],
+                           env=env, check=True, timeout=300)
+            res.append(np.load(out))
+        assert np.abs(res[0] - res[1]).max() <= 1e-12
+        outs.append(res)
 
 
 def test_kick_step_out_of_range_is_no_kick():
@@ -480,3 +534,89 @@ def test_strict_work_counters():
     assert 0 < c["working_set_slots"] < c["instance_passes"] * 150
     assert c["wave_passes"] * 64 >= c["instance_passes"]
     assert p.counters()["launches"] == 0
+
+
+# ------------------------------------------------ strict: long horizons, Cholesky cross-check
+
+
+def test_strict_long_horizon_rollout_vs_oracle():
+    """N = 400: the LQ kernel with 4 waves per workgroup (8 waves' slot flags exceed LDS);
+    300 samples of the stepping phase, 800 N kick (tests/golden/strict_long_oracle.npz)."""
+    d = golden("strict_long_oracle.npz")
+    N = 400
+    zx, zn = d["n400_zmax"], d["n400_zmin"]
+    n = len(zx)
+    x0 = np.stack([d["n400_x0"], d["n400_y0"]])[None]
+    p = plan(N, strict=True)
+    hist, st = p.rollout(zx, zn, x0, kick=np.array([float(d["n400_kick"])]), kick_step=n // 2)
+    assert int(st.abs().max()) == 0
+    h = hist.cpu().numpy()[0]
+    ref = d["n400_hist"]
+    assert rmse(h[:, :, 0], ref[:, :, 0]) <= 1e-9
+    assert np.abs(h - ref).max() <= 1e-6
+
+
+@pytest.mark.parametrize("N", (400, 700, 1300))
+def test_strict_long_horizon_step_vs_oracle(N):
+    """Cold-start strict solves at horizons run with 4, 2 and 1 waves per workgroup."""
+    d = golden("strict_long_oracle.npz")
+    p = plan(N, strict=True)
+    out, st = p.step(d[f"step{N}_x"], d[f"step{N}_zmax"], d[f"step{N}_zmin"])
+    ref = d[f"step{N}_out"]
+    assert int(st.abs().max()) == 0
+    assert np.abs(out.cpu().numpy() - ref).max() <= 1e-7 * max(1.0, np.abs(ref).max())
+
+
+def test_strict_horizon_limit():
+    with pytest.raises(ValueError, match="strict horizon"):
+        plan(2561, strict=True)
+
+
+_CHOL_CHILD = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, sys.argv[1])
+from mpc_bipedal.solver import Plan
+s = np.load(sys.argv[2]); l = np.load(sys.argv[3])
+def rmse(a, b): return float(np.sqrt(np.mean((np.asarray(a) - np.asarray(b)) ** 2)))
+errs = {}
+for N in (64, 150):
+    zx, zn = s[f"n{N}_zmax"], s[f"n{N}_zmin"]
+    n = len(zx); dt = 1.5 / N
+    p = Plan(0, N, dt, 0.75, 9.81, 1.0, 1e-6, True)
+    for F in (0, 400, 800):
+        h, st = p.rollout(zx, zn, np.zeros((1, 2, 3)), kick=np.array([dt * F / 40.0]),
+                          kick_step=n // 2)
+        assert int(st.abs().max()) == 0
+        errs[f"n{N}_F{F}"] = rmse(h.cpu().numpy()[0][:, :, 0], s[f"n{N}_F{F}_hist"][:, :, 0])
+    out, st = p.step(s[f"step{N}_x"], s[f"step{N}_zmax"], s[f"step{N}_zmin"])
+    ref = s[f"step{N}_out"]
+    errs[f"step{N}"] = float(np.abs(out.cpu().numpy() - ref).max() / max(1.0, np.abs(ref).max()))
+p = Plan(0, 400, 1.5 / 400, 0.75, 9.81, 1.0, 1e-6, True)
+zx, zn = l["n400_zmax"], l["n400_zmin"]; n = len(zx)
+x0 = np.stack([l["n400_x0"], l["n400_y0"]])[None]
+h, st = p.rollout(zx, zn, x0, kick=np.array([float(l["n400_kick"])]), kick_step=n // 2)
+assert int(st.abs().max()) == 0
+errs["n400"] = rmse(h.cpu().numpy()[0][:, :, 0], l["n400_hist"][:, :, 0])
+out, st = p.step(l["step400_x"], l["step400_zmax"], l["step400_zmin"])
+ref = l["step400_out"]
+errs["step400"] = float(np.abs(out.cpu().numpy() - ref).max() / max(1.0, np.abs(ref).max()))
+print(errs)
+for k, v in errs.items():
+    assert v <= (1e-7 if k.startswith("step") else 1e-6), (k, v)
+print("CHOL_OK")
+"""
+
+
+def test_strict_cholesky_variant_vs_oracle():
+    """The reduced-Cholesky strict kernel (strict.hip, ZMPC_STRICT_VARIANT=chol — a cross-check
+    of the default LQ kernel) on the N = 64/150 walks and single solves and on the N = 400
+    long-horizon fixtures (its 320 < N <= 512 range)."""
+    import subprocess
+    import sys
+    env = dict(os.environ, ZMPC_STRICT_VARIANT="chol")
+    r = subprocess.run([sys.executable, "-c", _CHOL_CHILD, PKG,
+                        os.path.join(os.path.dirname(__file__), "golden", "strict_oracle.npz"),
+                        os.path.join(os.path.dirname(__file__), "golden",
+                                     "strict_long_oracle.npz")],
+                       env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and "CHOL_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
