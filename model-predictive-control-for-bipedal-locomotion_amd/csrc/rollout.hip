@@ -1287,6 +1287,11 @@ void launch_unc(const RolloutGeom& g, size_t lds, hipStream_t s, const RolloutAr
             &per_cu, reinterpret_cast<const void*>(zmpc_rollout_unc_pers_kernel<CW>), 128,
             lds_split) != hipSuccess)
       per_cu = 0;
+    static const int per_cu_env = [] {
+      const char* e = getenv("ZMPC_PERS_PER_CU");  // A/B only: resident workgroups per CU
+      return e ? atoi(e) : 0;
+    }();
+    if (per_cu_env > 0) per_cu = std::min(per_cu, per_cu_env);
     const int64_t grid = (int64_t)std::max(g_cus, 1) * per_cu;
     // persistent only for a few walks per workgroup: config 2 (2 per workgroup) 45 µs vs
     // 49 µs; at 8 per workgroup (B = 16384) the one-walk grid is faster (156 vs 177 µs)
