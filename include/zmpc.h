@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define ZMPC_ABI_VERSION 3
+#define ZMPC_ABI_VERSION 4
 
 /* return codes */
 #define ZMPC_OK 0
@@ -144,6 +144,54 @@ int zmpc_rollout_kicks(const zmpc_plan* plan, int64_t B, int64_t n, const double
 int zmpc_cop_generate(int device, int64_t B, const double* params, int64_t n_cap,
                       double* zmax, double* zmin, int8_t* states, int64_t* n_out,
                       void* stream);
+
+/*
+ * Herdt joint footstep QP (config.method == "herdt"), since ABI 4.
+ * The plan supplies N (horizon) and the LIPM constants (dt, h, g); its strict flag is unused.
+ * Support states are int8: 0 STANDING, 1 DOUBLE_SUPPORT, 2 SINGLE_SUPPORT (cop_generator.py:11-15).
+ */
+#define ZMPC_HERDT_MAX_FACETS 16
+typedef struct zmpc_herdt_params {
+  double alpha, beta, gamma;         /* cost weights (config.py:42-45) */
+  double foot_length, foot_width;    /* ZMP box around the foot centre: ±½·dim (:666, :680) */
+  double foot_spread;                /* initial y foot position, standing hull (:457, :726-731) */
+  int32_t nfacets[2];                /* facets of the left / right swing polytope */
+  double facets[2][ZMPC_HERDT_MAX_FACETS][3]; /* (a_x, a_y, b): a·(f − f_current) <= b, the
+                                        reference's _polytope_halfspace (:828-865) */
+  int32_t max_footsteps;             /* most footsteps (support segments after the current
+                                        one) inside any horizon window of the batch, <= 8 */
+} zmpc_herdt_params;
+
+/*
+ * Batched ZMPController.generate_com_trajectory_herdt (zmp_controller.py:435-531) over
+ * predict_herdt_joint (:533-826) for B walks of n samples (exact QP solution; the reference's
+ * cvxpy/OSQP result differs by up to OSQP's tolerances).
+ *   v_ref [B, n, 2] reference velocities (v_stride doubles between walks, 0 = shared)
+ *   states [B, n] int8 (s_stride bytes between walks, 0 = shared)
+ *   nb_next [B, n] int32: find_nb_steps(padded states)[i][0] (:470), the divisor of the
+ *            air-foot interpolation (:497-500) (nb_stride elements between walks, 0 = shared)
+ *   x0 [B, 2, 3] initial (x, y) states; kick [B] or NULL: y-velocity impulse dt·F_ext/m
+ *            subtracted at step kick_step (:525-526)
+ *   hist [B, n, 2, 3] state history; foot [B, n, 2] foot positions (foot_hist, :529-530)
+ */
+int zmpc_herdt_rollout(const zmpc_plan* plan, const zmpc_herdt_params* params, int64_t B,
+                       int64_t n, const double* v_ref, int64_t v_stride, const int8_t* states,
+                       int64_t s_stride, const int32_t* nb_next, int64_t nb_stride,
+                       const double* x0, const double* kick, int64_t kick_step, double* hist,
+                       double* foot, int32_t* status, void* stream);
+
+/*
+ * Batched predict_herdt_joint (zmp_controller.py:533-826), one QP per instance, cold start:
+ *   x [B, 2, 3] (x, y) states; v_win [B, N, 2] window of v_ref; s_win [B, N] window states;
+ *   current [B] int8 current support state; foot [B, 2] current foot (x_fc, y_fc);
+ *   side [B] int8 (0 left, 1 right)
+ *   → x_next [B, 2, 3]; step [B, 2] first planned footstep (NaN when the window holds none,
+ *     the reference's None).
+ */
+int zmpc_herdt_step(const zmpc_plan* plan, const zmpc_herdt_params* params, int64_t B,
+                    const double* x, const double* v_win, const int8_t* s_win,
+                    const int8_t* current, const double* foot, const int8_t* side,
+                    double* x_next, double* step, int32_t* status, void* stream);
 
 /* Message describing the last failure on the calling thread ("" if none). */
 const char* zmpc_last_error(void);

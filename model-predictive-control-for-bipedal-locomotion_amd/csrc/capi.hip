@@ -86,6 +86,7 @@ int zmpc_plan_create(int device, int32_t N, double T, double T2_2, double T3_6, 
     if ((e = zmpc_rollout_unc_set_attrs()) != hipSuccess) return hip_fail(e, "set LDS attrs");
     if ((e = zmpc_strict_set_attrs()) != hipSuccess) return hip_fail(e, "set LDS attrs");
     if ((e = zmpc_strict_lq_set_attrs()) != hipSuccess) return hip_fail(e, "set LDS attrs");
+    if ((e = zmpc_herdt_set_attrs()) != hipSuccess) return hip_fail(e, "set LDS attrs");
     // the strict solvers' per-launch workspaces come from the stream-ordered pool: keep up to
     // ZMPC_POOL_KEEP_MB (default 4096) of freed blocks in the pool across synchronisations
     // instead of returning them to the driver every time; anything above is released
@@ -296,6 +297,69 @@ int zmpc_rollout_kicks(const zmpc_plan* P, int64_t B, int64_t n, const double* z
   }
   return rollout_impl(P, B, n, zmax, zmin, bounds_stride, x0, kick, -1, kick_steps, hist,
                       status, stream);
+}
+
+static int herdt_check(const zmpc_plan* P, const zmpc_herdt_params* prm, int64_t B) {
+  if (!P || !prm) return fail(ZMPC_EINVAL, "NULL plan or params");
+  if (B < 0) return fail(ZMPC_EINVAL, "B < 0");
+  for (int sd = 0; sd < 2; ++sd)
+    if (prm->nfacets[sd] < 3 || prm->nfacets[sd] > ZMPC_HERDT_MAX_FACETS)
+      return fail(ZMPC_EINVAL, "polytope facets must be in [3, 16]");
+  if (prm->max_footsteps < 0 || prm->max_footsteps > 8)
+    return fail(ZMPC_EINVAL, "max_footsteps must be in [0, 8]");
+  if (!(prm->alpha > 0) || !(prm->beta >= 0) || !(prm->gamma > 0))
+    return fail(ZMPC_EINVAL, "need alpha > 0, beta >= 0, gamma > 0");
+  return ZMPC_OK;
+}
+
+int zmpc_herdt_rollout(const zmpc_plan* P, const zmpc_herdt_params* prm, int64_t B, int64_t n,
+                       const double* v_ref, int64_t v_stride, const int8_t* states,
+                       int64_t s_stride, const int32_t* nb_next, int64_t nb_stride,
+                       const double* x0, const double* kick, int64_t kick_step, double* hist,
+                       double* foot, int32_t* status, void* stream) {
+  g_err.clear();
+  int rc = herdt_check(P, prm, B);
+  if (rc != ZMPC_OK) return rc;
+  if (n < 1) return fail(ZMPC_EINVAL, "need n >= 1");
+  if (B == 0) return ZMPC_OK;
+  if (!v_ref || !states || !nb_next || !x0 || !hist || !foot)
+    return fail(ZMPC_EINVAL, "NULL array argument");
+  if (B > 0x7fffffff || n > (1 << 24)) return fail(ZMPC_EINVAL, "batch too large");
+  if ((v_stride != 0 && v_stride < 2 * n) || (s_stride != 0 && s_stride < n) ||
+      (nb_stride != 0 && nb_stride < n))
+    return fail(ZMPC_EINVAL, "strides must be 0 (shared) or cover a whole walk");
+  DeviceGuard g(P->device);
+  if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
+  hipStream_t s = (hipStream_t)stream;
+  if (status) {
+    hipError_t e = hipMemsetAsync(status, 0, sizeof(int32_t) * B, s);
+    if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync");
+  }
+  std::string why;
+  hipError_t e = zmpc_launch_herdt(P, prm, B, n, 0, v_ref, v_stride, states, s_stride, nb_next,
+                                   nb_stride, x0, kick, kick_step, nullptr, nullptr, nullptr,
+                                   hist, foot, status, s, &why);
+  return launch_result(e, why, "zmpc_herdt_rollout");
+}
+
+int zmpc_herdt_step(const zmpc_plan* P, const zmpc_herdt_params* prm, int64_t B,
+                    const double* x, const double* v_win, const int8_t* s_win,
+                    const int8_t* current, const double* foot, const int8_t* side,
+                    double* x_next, double* step, int32_t* status, void* stream) {
+  g_err.clear();
+  int rc = herdt_check(P, prm, B);
+  if (rc != ZMPC_OK) return rc;
+  if (B == 0) return ZMPC_OK;
+  if (!x || !v_win || !s_win || !current || !foot || !side || !x_next || !step)
+    return fail(ZMPC_EINVAL, "NULL array argument");
+  if (B > 0x7fffffff) return fail(ZMPC_EINVAL, "batch too large");
+  DeviceGuard g(P->device);
+  if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
+  std::string why;
+  hipError_t e = zmpc_launch_herdt(P, prm, B, 1, 1, v_win, 2 * (int64_t)P->N, s_win, P->N,
+                                   nullptr, 0, x, nullptr, -1, current, foot, side, x_next, step,
+                                   status, (hipStream_t)stream, &why);
+  return launch_result(e, why, "zmpc_herdt_step");
 }
 
 int zmpc_cop_generate(int device, int64_t B, const double* params, int64_t n_cap,

@@ -99,6 +99,17 @@ hipError_t zmpc_strict_lq_set_attrs();
 size_t zmpc_strict_lq_table_doubles(int N);
 hipError_t zmpc_strict_lq_build_table(zmpc_plan* p, hipStream_t s);
 
+// Herdt joint footstep QP (herdt.hip); support states as cop_generator.State
+constexpr int ZMPC_STANDING = 0, ZMPC_DOUBLE_SUPPORT = 1, ZMPC_SINGLE_SUPPORT = 2;
+hipError_t zmpc_launch_herdt(const zmpc_plan* p, const zmpc_herdt_params* prm, int64_t B,
+                             int64_t n, int window_mode, const double* vref, int64_t vs,
+                             const int8_t* st, int64_t ss, const int32_t* nb, int64_t ns,
+                             const double* x0, const double* kick, int64_t kick_step,
+                             const int8_t* cur0, const double* fc0, const int8_t* side0,
+                             double* hist, double* foot, int32_t* status, hipStream_t s,
+                             std::string* why);
+hipError_t zmpc_herdt_set_attrs();
+
 hipError_t zmpc_rollout_unc_set_attrs();
 hipError_t zmpc_strict_set_attrs();
 

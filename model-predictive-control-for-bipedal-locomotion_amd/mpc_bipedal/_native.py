@@ -12,8 +12,9 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ZMPC_LIB", os.path.join(_HERE, "libzmpc.so"))
 
-ABI_VERSION = 3  # include/zmpc.h ZMPC_ABI_VERSION this binding is written for
+ABI_VERSION = 4  # include/zmpc.h ZMPC_ABI_VERSION this binding is written for
 NCOUNTERS = 4    # include/zmpc.h ZMPC_NCOUNTERS
+HERDT_MAX_FACETS = 16  # include/zmpc.h ZMPC_HERDT_MAX_FACETS
 
 ZMPC_OK = 0
 ZMPC_EINVAL = -1
@@ -54,6 +55,16 @@ SIGNATURES = {
     "zmpc_cop_generate": (ctypes.c_int, [ctypes.c_int, ctypes.c_int64, _c_dbl_p, ctypes.c_int64,
                                          _c_dbl_p, _c_dbl_p, ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.c_void_p]),
+    # params: const zmpc_herdt_params* (a ctypes.Structure passed byref)
+    "zmpc_herdt_rollout": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                          ctypes.c_int64, _c_dbl_p, ctypes.c_int64,
+                                          ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                                          ctypes.c_int64, _c_dbl_p, _c_dbl_p, ctypes.c_int64,
+                                          _c_dbl_p, _c_dbl_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "zmpc_herdt_step": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                       _c_dbl_p, _c_dbl_p, ctypes.c_void_p, ctypes.c_void_p,
+                                       _c_dbl_p, ctypes.c_void_p, _c_dbl_p, _c_dbl_p,
+                                       ctypes.c_void_p, ctypes.c_void_p]),
 }
 
 _lib = None

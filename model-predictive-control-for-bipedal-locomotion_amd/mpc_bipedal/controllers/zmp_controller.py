@@ -7,9 +7,12 @@ QP solve runs in hand-written HIP kernels (``csrc/``) reached through the C-ABI 
 ``include/zmpc.h``; NumPy inputs are staged to the device and results copied back, which is
 the only host work.  There is no CPU solver behind this class.
 
+The Herdt joint footstep QP (``method="herdt"``, :203-531) runs on the device as well
+(``csrc/herdt.hip``); its host bookkeeping is in ``controllers/herdt.py``.
+
 Additions (not in the reference): ``generate_com_trajectory_batch`` /
-``generate_state_trajectory_batch`` for many walks or disturbance scenarios at once, taking
-and returning torch device tensors.
+``generate_state_trajectory_batch`` / ``generate_com_trajectory_herdt_batch`` for many walks or
+disturbance scenarios at once, taking and returning torch device tensors.
 """
 
 from typing import Optional, Tuple
@@ -20,6 +23,7 @@ import torch
 from ..config import MPCConfig
 from ..models.lipm_model import lipm_matrices
 from ..solver import get_plan
+from . import herdt
 
 _FAILED = "QP solver did not find a solution (infeasible or other)."
 
@@ -108,14 +112,93 @@ class ZMPController:
             self._raise_on_status(st)
         return out.cpu().numpy().reshape(3, 1)
 
-    # ------------------------------------------------------------------ Herdt (out of scope)
-    def generate_com_trajectory_herdt(self, *args, **kwargs):
-        """Herdt joint footstep QP (zmp_controller.py:435-531): not part of this solver."""
-        raise NotImplementedError("method='herdt' is not implemented by the HIP solver "
-                                  "(only the Wieber QP is accelerated)")
+    # ------------------------------------------------------------------ Herdt
+    def find_nb_steps(self, state_ref) -> list:
+        """(steps to the next footstep change, steps of the current footstep phase) per index
+        (zmp_controller.py:203-433)."""
+        return herdt.find_nb_steps(state_ref)
 
-    def predict_herdt_joint(self, *args, **kwargs):
-        raise NotImplementedError("method='herdt' is not implemented by the HIP solver")
+    def _polytope_halfspace(self, vertices):
+        """Convex polygon → (A, b) with A d <= b (zmp_controller.py:828-865)."""
+        return herdt.polytope_halfspace(vertices)
+
+    def generate_com_trajectory_herdt(self, x_init: np.ndarray, y_init: np.ndarray,
+                                      v_ref: np.ndarray, state_ref: np.ndarray):
+        """COM trajectory (n,2), y state history (n,3,1) and foot positions (n,2) of the Herdt
+        joint footstep QP (zmp_controller.py:435-531), every QP on the device."""
+        v_ref = np.asarray(v_ref, dtype=np.float64)
+        n = len(v_ref)
+        x0 = np.stack([np.asarray(x_init, np.float64).reshape(3),
+                       np.asarray(y_init, np.float64).reshape(3)])[None]
+        kick = np.array([self._kick()]) if self.config.add_force else None
+        hist, foot = self._herdt_rollout(x0, v_ref, herdt.encode_states(state_ref), kick, n // 2)
+        hist, foot = hist[0].cpu().numpy(), foot[0].cpu().numpy()
+        for i in np.nonzero(np.any(foot[1:] != foot[:-1], axis=1))[0]:
+            # zmp_controller.py:510 (the footstep adopted when a single support ends)
+            print(f"Je change : de ({foot[i, 0], foot[i, 1]}) à ({foot[i + 1, 0], foot[i + 1, 1]})")
+        com = hist[:, :, 0].copy()
+        return com, hist[:, 1, :].reshape(n, 3, 1).copy(), foot
+
+    def predict_herdt_joint(self, x_init, y_init, v_ref, x_fc, y_fc, current_state, state_ref,
+                            nb_steps, nb_steps_to_next_state, x_airc, y_airc, foot_side, idx):
+        """One joint x/y step (zmp_controller.py:533-826): (next x state (3,1), next y state
+        (3,1), first planned x footstep or None, first planned y footstep or None).  The
+        solver is exact, so the reference's fallback to the air foot (:796-802) never runs."""
+        plan = self._plan(nb_steps)
+        v = np.asarray(v_ref, np.float64).reshape(1, nb_steps, 2)
+        win = herdt.encode_states(state_ref).reshape(1, nb_steps)
+        cur = herdt.encode_states([current_state])
+        pad = herdt.pad_states(np.concatenate([cur, win[0]]), 0)[None]
+        prm = herdt.make_params(self.config, herdt.max_footsteps(pad, nb_steps, 2))
+        x = np.stack([np.asarray(x_init, np.float64).reshape(3),
+                      np.asarray(y_init, np.float64).reshape(3)])[None]
+        foot = np.array([[float(np.asarray(x_fc).reshape(-1)[0]),
+                          float(np.asarray(y_fc).reshape(-1)[0])]])
+        side = np.array([0 if foot_side == "left" else 1], np.int8)
+        xn, step, st = plan.herdt_step(prm, x, v, win, cur, foot, side)
+        self._raise_on_status(st)
+        xn, step = xn[0].cpu().numpy(), step[0].cpu().numpy()
+        fx = None if np.isnan(step[0]) else float(step[0])
+        fy = None if np.isnan(step[1]) else float(step[1])
+        return xn[0].reshape(3, 1), xn[1].reshape(3, 1), fx, fy
+
+    def generate_com_trajectory_herdt_batch(self, x_init, v_ref, state_ref, F_ext=None):
+        """Many Herdt walks at once (addition): x_init [B,2,3] or None; v_ref [B,n,2] or a
+        shared [n,2]; state_ref [B,n] or a shared [n] (State enums or int8 codes); F_ext [B]
+        or None.  Returns (com [B,n,2], hist [B,n,2,3], foot [B,n,2]) on the device."""
+        v = torch.as_tensor(v_ref, dtype=torch.float64)
+        n = int(v.shape[-2])
+        st = herdt.encode_states(state_ref) if not isinstance(state_ref, torch.Tensor) \
+            else state_ref.cpu().numpy().astype(np.int8)
+        if x_init is not None:
+            B = int(np.shape(x_init)[0])
+        elif v.dim() == 3:
+            B = int(v.shape[0])
+        elif st.ndim == 2:
+            B = int(st.shape[0])
+        else:
+            B = 1 if F_ext is None else int(np.size(F_ext))
+        x0 = np.zeros((B, 2, 3)) if x_init is None else x_init
+        kick = None
+        if F_ext is not None:
+            kick = self.config.dt * np.asarray(F_ext, np.float64).reshape(B) / self.config.m
+        hist, foot = self._herdt_rollout(x0, v_ref, st, kick, n // 2)
+        return hist[..., 0], hist, foot
+
+    def _herdt_rollout(self, x0, v_ref, st, kick, kick_step):
+        plan = self._plan()
+        N = plan.N
+        st2 = np.atleast_2d(st)
+        pad = np.concatenate([st2, np.repeat(st2[:, -1:], N, axis=1)], axis=1)
+        n = st2.shape[1]
+        prm = herdt.make_params(self.config, herdt.max_footsteps(pad, N, n))
+        nb = np.array([[t[0] for t in herdt.find_nb_steps(p)][:n] for p in pad], np.int32)
+        if st.ndim == 1:
+            nb = nb[0]
+        hist, foot, status = plan.herdt_rollout(prm, v_ref, st, nb, x0, kick=kick,
+                                                kick_step=kick_step)
+        self._raise_on_status(status)
+        return hist, foot
 
     # ------------------------------------------------------------------ batched additions
     def generate_state_trajectory_batch(self, x_init, z_max, z_min, F_ext=None,

@@ -179,6 +179,72 @@ class Plan:
         return hist, status, ("zmpc_rollout_kicks", args, (zmax, zmin, x0, kick_t, ks))
 
 
+    # -- Herdt joint footstep QP (zmpc_herdt_rollout / zmpc_herdt_step) --------------------
+    def herdt_rollout(self, params, v_ref, states, nb_next, x0, kick=None, kick_step=-1):
+        """Batched generate_com_trajectory_herdt → (hist [B,n,2,3], foot [B,n,2], status [B]).
+
+        v_ref [B,n,2] or a shared [n,2]; states [B,n] or [n] int8 codes; nb_next [B,n] or [n]
+        int32 (find_nb_steps of the padded states, first element); x0 [B,2,3]; kick [B] or
+        None: y-velocity impulse at kick_step.  params: controllers.herdt.HerdtParams.
+        """
+        x0 = self._as_dev(x0)
+        if x0.dim() != 3 or x0.shape[1:] != (2, 3):
+            raise ValueError(f"x0 must be [B, 2, 3], got {tuple(x0.shape)}")
+        B = int(x0.shape[0])
+        v = self._as_dev(v_ref)
+        n = int(v.shape[-2])
+        if v.dim() == 2:
+            vs = 0
+        elif v.dim() == 3 and v.shape[0] == B:
+            vs = 2 * n
+        else:
+            raise ValueError(f"v_ref must be [B, n, 2] or [n, 2], got {tuple(v.shape)}")
+        dev = self._dev()
+        st = torch.as_tensor(np.asarray(states, dtype=np.int8) if not isinstance(
+            states, torch.Tensor) else states, dtype=torch.int8, device=dev).contiguous()
+        nb = torch.as_tensor(np.asarray(nb_next, dtype=np.int32) if not isinstance(
+            nb_next, torch.Tensor) else nb_next, dtype=torch.int32, device=dev).contiguous()
+        ss = 0 if st.dim() == 1 else n
+        ns = 0 if nb.dim() == 1 else n
+        if st.shape[-1] != n or nb.shape[-1] != n:
+            raise ValueError("states and nb_next must hold n samples per walk")
+        kick_t = None if kick is None else self._as_dev(kick, (B,))
+        hist = torch.empty((B, n, 2, 3), dtype=torch.float64, device=dev)
+        foot = torch.empty((B, n, 2), dtype=torch.float64, device=dev)
+        status = torch.empty(B, dtype=torch.int32, device=dev)
+        with torch.cuda.device(self.device):
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+            rc = _native.load().zmpc_herdt_rollout(
+                self._h, ctypes.byref(params), B, n, _ptr(v), vs, _ptr(st), ss, _ptr(nb), ns,
+                _ptr(x0), _ptr(kick_t), int(kick_step), _ptr(hist), _ptr(foot), _ptr(status),
+                ctypes.c_void_p(stream))
+        _native.check(rc, "zmpc_herdt_rollout")
+        return hist, foot, status
+
+    def herdt_step(self, params, x, v_win, s_win, current, foot, side):
+        """Batched predict_herdt_joint: x [B,2,3], v_win [B,N,2], s_win [B,N] int8,
+        current [B] int8, foot [B,2], side [B] int8 (0 left) → (x_next [B,2,3],
+        first footstep [B,2] (NaN: none), status [B])."""
+        x = self._as_dev(x)
+        B = int(x.shape[0])
+        dev = self._dev()
+        v = self._as_dev(v_win, (B, self.N, 2))
+        f = self._as_dev(foot, (B, 2))
+        i8 = lambda a, shape: torch.as_tensor(np.asarray(a, dtype=np.int8).reshape(shape),
+                                              device=dev).contiguous()
+        sw, cu, sd = i8(s_win, (B, self.N)), i8(current, (B,)), i8(side, (B,))
+        xn = torch.empty((B, 2, 3), dtype=torch.float64, device=dev)
+        step = torch.empty((B, 2), dtype=torch.float64, device=dev)
+        status = torch.empty(B, dtype=torch.int32, device=dev)
+        with torch.cuda.device(self.device):
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+            rc = _native.load().zmpc_herdt_step(
+                self._h, ctypes.byref(params), B, _ptr(x), _ptr(v), _ptr(sw), _ptr(cu), _ptr(f),
+                _ptr(sd), _ptr(xn), _ptr(step), _ptr(status), ctypes.c_void_p(stream))
+        _native.check(rc, "zmpc_herdt_step")
+        return xn, step, status
+
+
 def get_plan(config, device=None) -> Plan:
     """Cached plan for an MPCConfig (keyed on every field the hot path reads)."""
     dev = _device_index(getattr(config, "backend", "hip")) if device is None else int(device)

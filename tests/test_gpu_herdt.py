@@ -1,0 +1,106 @@
+"""Parity of the device Herdt joint footstep QP (csrc/herdt.hip, through the C-ABI) with the
+reference-driven golden vectors (tests/golden/herdt_default.npz: the reference's own Herdt code
+with each QP solved exactly — see tests/golden/make_herdt_golden.py; parity with OSQP unpinned)
+and with the CPU oracle (oracle/herdt_oracle.py).
+
+Tolerances: the reference and the device compute the same exact optimum in FP64; CoM RMSE
+<= 1e-9 and footsteps <= 1e-9 here (measured ≈1e-13), the north-star bar is 1e-6.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden, rmse
+from oracle import herdt_oracle as HO
+
+pytestmark = pytest.mark.gpu
+
+from mpc_bipedal.config import MPCConfig  # noqa: E402
+from mpc_bipedal.controllers import ZMPController  # noqa: E402
+from mpc_bipedal.controllers import herdt as H  # noqa: E402
+
+
+@pytest.fixture(scope="module", autouse=True)
+def need_gpu():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a HIP device")
+
+
+def test_herdt_rollout_vs_reference():
+    """generate_com_trajectory (method='herdt', add_force) on the default walk: CoM, y state
+    history and foot positions vs the reference-driven rollout."""
+    d = golden("herdt_default.npz")
+    c = ZMPController(MPCConfig(method="herdt", add_force=True))
+    com, y_hist, foot = c.generate_com_trajectory(np.zeros((3, 1)), np.zeros((3, 1)),
+                                                  v_ref=d["v_ref"], state_ref=d["states"])
+    assert com.shape == d["com"].shape and y_hist.shape == (len(com), 3, 1)
+    assert rmse(com, d["com"]) <= 1e-9
+    assert np.abs(foot - d["foot_hist"]).max() <= 1e-9
+    assert np.abs(y_hist[:, :, 0] - d["y_hist"]).max() <= 1e-8
+    zmp = y_hist[:, :, 0] @ c.C
+    assert rmse(zmp, d["y_hist"] @ c.C) <= 1e-9
+
+
+def test_herdt_steps_vs_reference():
+    """predict_herdt_joint on the saved steps (footsteps in the window: m = 0 .. 7)."""
+    d = golden("herdt_default.npz")
+    c = ZMPController(MPCConfig(method="herdt"))
+    A, B = c.A, c.B
+    for k in range(int(d["n_steps_saved"])):
+        g = lambda key: d[f"step{k}_{key}"]
+        N, m = int(g("N")), int(g("m"))
+        side = "left" if int(g("side")) == 0 else "right"
+        xn, yn, fx, fy = c.predict_herdt_joint(g("x"), g("y"), g("v"), g("fx"), g("fy"),
+                                               int(g("cur")), g("win"), N, (1, 1), None, None,
+                                               side, k)
+        sol = g("sol")
+        assert np.abs(xn - (A @ g("x").reshape(3, 1) + B * sol[0])).max() <= 1e-9, k
+        assert np.abs(yn - (A @ g("y").reshape(3, 1) + B * sol[N + m])).max() <= 1e-9, k
+        if m == 0:
+            assert fx is None and fy is None
+        else:
+            assert abs(fx - sol[N]) <= 1e-9 and abs(fy - sol[2 * N + m]) <= 1e-9, k
+
+
+def test_herdt_batch_force_sweep():
+    """Batched rollout of one walk under an F_ext sweep (shared v_ref/states): the 400 N walk
+    equals the single-walk reference rollout, F = 0 equals the oracle without force (short
+    walk), every walk converges."""
+    d = golden("herdt_default.npz")
+    c = ZMPController(MPCConfig(method="herdt", add_force=True))
+    F = np.array([0.0, 200.0, 400.0, 800.0] * 16)
+    com, hist, foot = c.generate_com_trajectory_herdt_batch(None, d["v_ref"], d["states"],
+                                                            F_ext=F)
+    com = com.cpu().numpy()
+    assert com.shape == (64,) + d["com"].shape
+    assert rmse(com[2], d["com"]) <= 1e-9 and rmse(com[62], d["com"]) <= 1e-9
+    assert np.array_equal(com[0], com[4]) and np.array_equal(com[3], com[63])
+    # no force: x axis identical to the forced walks' x axis until the kick
+    n = d["com"].shape[0]
+    assert np.abs(com[0, : n // 2 + 1] - com[2, : n // 2 + 1]).max() <= 1e-12
+
+
+def test_herdt_short_walk_vs_oracle():
+    """A short ragged walk (a stepping window of the default schedule, velocities 0.2 m/s,
+    start mid-walk at rest) against the oracle's own rollout."""
+    d = golden("herdt_default.npz")
+    st = d["states"][100:190].copy()
+    v = np.zeros((len(st), 2))
+    v[:, 0] = np.where(st == 0, 0.0, 0.2)
+    cfg = MPCConfig(method="herdt", add_force=True, F_ext=300.0)
+    com_o, y_o, foot_o, _ = HO.herdt_rollout(cfg, np.zeros(3), np.zeros(3), v, st)
+    c = ZMPController(cfg)
+    com, y_hist, foot = c.generate_com_trajectory(np.zeros((3, 1)), np.zeros((3, 1)),
+                                                  v_ref=v, state_ref=st)
+    assert rmse(com, com_o) <= 1e-9
+    assert np.abs(foot - foot_o).max() <= 1e-9
+
+
+def test_herdt_find_nb_steps_drop_in():
+    d = golden("herdt_default.npz")
+    c = ZMPController(MPCConfig(method="herdt"))
+    st = d["states"]
+    pad = np.concatenate([st, np.repeat(st[-1:], 150)])
+    assert np.array_equal(np.array(c.find_nb_steps(pad)), d["nb_steps"])
+    A, b = c._polytope_halfspace(np.array(MPCConfig().left_foot_polytope))
+    assert np.array_equal(A, d["poly_left_A"])

@@ -92,7 +92,7 @@ def test_library_loads_and_exports_every_symbol():
     exported = set(re.findall(r" T (zmpc_\w+)", out))
     assert set(_header_symbols()) <= exported
     lib = _native.load()
-    assert lib.zmpc_abi_version() == _native.ABI_VERSION == 3
+    assert lib.zmpc_abi_version() == _native.ABI_VERSION == 4
     assert lib.zmpc_last_error() == b""
 
 
@@ -118,6 +118,12 @@ def test_argument_errors_without_gpu():
     buf = (ctypes.c_uint64 * _native.NCOUNTERS)()
     rc = lib.zmpc_plan_counters(None, buf, _native.NCOUNTERS, 0)
     assert rc == _native.ZMPC_EINVAL and b"NULL" in lib.zmpc_last_error()
+    rc = lib.zmpc_herdt_rollout(None, None, 1, 10, None, 0, None, 0, None, 0, None, None, -1,
+                                None, None, None, None)
+    assert rc == _native.ZMPC_EINVAL and b"NULL" in lib.zmpc_last_error()
+    rc = lib.zmpc_herdt_step(None, None, 1, None, None, None, None, None, None, None, None,
+                             None, None)
+    assert rc == _native.ZMPC_EINVAL
 
 
 def test_router_errors():
@@ -128,9 +134,11 @@ def test_router_errors():
     c2 = ZMPController(MPCConfig(method="herdt"))
     with pytest.raises(ValueError, match="v_ref and state_ref"):
         c2.generate_com_trajectory(np.zeros((3, 1)), np.zeros((3, 1)))
-    with pytest.raises(NotImplementedError):
-        c2.generate_com_trajectory(np.zeros((3, 1)), np.zeros((3, 1)), v_ref=np.zeros(3),
-                                   state_ref=[])
+    if not __import__("torch").cuda.is_available():
+        # the Herdt QP runs on the device only: no CPU fallback behind the drop-in
+        with pytest.raises(RuntimeError, match="HIP device"):
+            c2.generate_com_trajectory(np.zeros((3, 1)), np.zeros((3, 1)),
+                                       v_ref=np.zeros((5, 2)), state_ref=[0] * 5)
     c3 = ZMPController(MPCConfig(method="foo"))
     with pytest.raises(ValueError, match="Unknown method"):
         c3.generate_com_trajectory(np.zeros((3, 1)), np.zeros((3, 1)))
