@@ -11,6 +11,11 @@ Workloads (`--config`, default 2 = BASELINE.json's metric config
      (bounds_stride 0), x0 = 0, F ~ U(0, 800) N, strict; per GPU 125 000 scenarios
      (`--unconstrained` for the unconstrained variant).
   5  horizon N = 512 (dt = 1.5/512, n = 1431), offsets as 2, unconstrained, per GPU 2048.
+  6  Herdt joint footstep QP (method = "herdt"): the reference's default
+     Herdt walk (MPCConfig defaults, classic speed references, n = 302) shared by every walk,
+     x0 position ~ U(−0.01, 0.01) per axis, F_ext ~ U(0, 800) N at n//2; per GPU B = 32768
+     (one (walk, axis) per lane: 1024 waves, one per SIMD);
+     one solve = one joint x/y QP (predict_herdt_joint).
 One "step" = one batched rollout of every walk over all n−1 timesteps and both axes
 = B·(n−1)·2 QP solves, inputs already resident in HBM.
 
@@ -61,7 +66,159 @@ CONFIGS = {
     3: dict(batch=65536, horizon=150, strict=True, shared=False),
     4: dict(batch=125000, horizon=150, strict=True, shared=True),
     5: dict(batch=2048, horizon=512, strict=False, shared=False),
+    6: dict(batch=32768, horizon=150, strict=False, shared=True, herdt=True),
 }
+
+
+def rollout_kernel_name(B, n, N, strict):
+    """Which kernel zmpc_rollout launches for this shape (csrc/rollout.hip launch rules)."""
+    if strict:
+        return "zmpc_strict_lq_kernel"
+    if n - 1 <= 512:
+        slots = 8 * torch.cuda.get_device_properties(0).multi_processor_count
+        return ("zmpc_rollout_unc_pers_kernel" if slots < B <= 3 * slots
+                else "zmpc_rollout_unc_split_kernel")
+    return "zmpc_rollout_unc_wide_kernel" if n - 1 <= 4096 else "zmpc_rollout_unc_chunk_kernel"
+
+
+def herdt_bench(args, rank, world, dev):
+    """config 6: batched Herdt rollouts (csrc/herdt.hip); returns the JSON line (rank 0)."""
+    from mpc_bipedal.controllers import herdt as H
+    from mpc_bipedal.generators import SpeedTrajectoryGenerator
+    cfg = MPCConfig(method="herdt", add_force=True, horizon=args.horizon or 150)
+    B = args.batch or CONFIGS[6]["batch"]
+    vx, vy, states = SpeedTrajectoryGenerator(cfg).generate_speed_and_state(save_footsteps=False)
+    v_ref = np.stack([vx, vy], 1)
+    st = H.encode_states(states)
+    n, N = len(st), cfg.horizon
+    pad = H.pad_states(st, N)
+    nb = np.array([t[0] for t in H.find_nb_steps(pad)][:n], np.int32)
+    mmax = H.max_footsteps(pad[None], N, n)
+    prm = H.make_params(cfg, mmax)
+    rng = np.random.default_rng(SEED + 7919 * rank)
+    x0_h = np.zeros((B, 2, 3))
+    x0_h[:, :, 0] = rng.uniform(-0.01, 0.01, (B, 2))
+    F_h = rng.uniform(0.0, 800.0, B)
+    if rank == 0:
+        x0_h[0], F_h[0] = 0.0, cfg.F_ext   # the reference walk
+    kick_h = cfg.dt * F_h / cfg.m
+    plan = Plan(dev.index, N, cfg.dt, cfg.h, cfg.g, cfg.Q, cfg.R, False)
+    v = torch.as_tensor(v_ref, device=dev)
+    s_t = torch.as_tensor(st, device=dev)
+    nb_t = torch.as_tensor(nb, device=dev)
+    x0 = torch.as_tensor(x0_h, device=dev)
+    kick = torch.as_tensor(kick_h, device=dev)
+
+    def launch():
+        return plan.herdt_rollout(prm, v, s_t, nb_t, x0, kick=kick, kick_step=n // 2)
+    for _ in range(args.warmup):
+        launch()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        hist, foot, status = launch()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
+    assert int(status.abs().max()) == 0, "solver reported a failed instance"
+    solves_per_step = B * (n - 1) * world
+    value = solves_per_step * args.steps / elapsed
+    # minimal algorithmic FP64 work of one joint QP: one backward Riccati pass over the
+    # augmented state (3 + m) and one forward + costate sweep, both axes, at the window's
+    # footstep count m (mean over the walk); 2·NA² + 14·NA + 40 FLOP per row and axis for the
+    # value-function update (NA = 3 + m), 60 for forward + costate
+    a, b = pad[:-1].astype(np.int64), pad[1:].astype(np.int64)
+    brk = ((a != b) & ~((a == 1) & (b == 2))).astype(np.int64)   # footstep breaks (herdt.py)
+    cs = np.concatenate([[0], np.cumsum(brk)])
+    m_win = cs[np.arange(n - 1) + N] - cs[np.arange(n - 1)]      # footsteps per window
+    na = 3.0 + m_win
+    per_row = 2 * na ** 2 + 14 * na + 40 + 60
+    flops = float(B * 2 * N * per_row.sum())
+    tfs = flops / (kern_ms * 1e-3) / 1e12
+    if rank != 0:
+        return None
+    com_rmse_ref = None
+    gold = os.path.join(ROOT, "tests", "golden", "herdt_default.npz")
+    if os.path.exists(gold):
+        g = np.load(gold)
+        if g["com"].shape[0] == n:
+            com_rmse_ref = float(np.sqrt(np.mean((hist[0, :, :, 0].cpu().numpy() - g["com"])
+                                                 ** 2)))
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = _herdt_cpu_baseline(cfg, v_ref, st, hist.cpu().numpy(), foot.cpu().numpy(),
+                                  x0_h, kick_h, args.cpu_seconds)
+    return {
+        "metric": "QP solves/sec (horizon=150, batched) at 1/2/4/8 MI355X; CoM RMSE vs ref",
+        "value": value, "unit": "QP solves/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": "synthetic (the reference's default Herdt walk shared by every walk, seeded "
+                "x0/F_ext)",
+        "config": {"workload": f"config6: Herdt joint footstep QP, default walk, horizon={N}, "
+                               f"n={n}", "walks_per_gpu": B, "global_batch": B * world,
+                   "horizon": N, "samples_per_walk": n, "solves_per_step": solves_per_step,
+                   "parallelism": f"dp{world}", "max_footsteps_in_window": mmax,
+                   "solve": "one joint x/y QP (predict_herdt_joint, zmp_controller.py:533-826)"},
+        "roofline": {"bound": "mfma", "achieved": tfs, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
+                     "frac": tfs / FP64_PEAK_TFS, "traffic": None,
+                     "kernel": "zmpc_herdt_kernel", "kernel_ms": kern_ms,
+                     "alg_flops_per_launch": flops,
+                     "engine": "FP64 VALU, one (walk, axis) per lane; the FLOP count is one "
+                               "active-set pass (a lower bound)"},
+        "cpu_baseline": cpu, "com_rmse_vs_ref": com_rmse_ref}
+
+
+def _herdt_cpu_baseline(cfg, v_ref, st, hist_gpu, foot_gpu, x0_h, kick_h, budget_s):
+    """CPU leg for config 6 (rank 0): the oracle's exact Herdt rollout (herdt_oracle; the
+    reference's cvxpy/OSQP is not installed) on walk 0, timed for budget_s of CPU work (a
+    prefix of the walk), 1 process at the default BLAS threads; parity of the GPU walk 0."""
+    from oracle import herdt_oracle as HO
+    n = len(st)
+    N = cfg.horizon
+    vpad = np.vstack([v_ref, np.repeat(v_ref[-1:], N, axis=0)])
+    spad = np.concatenate([st, np.repeat(st[-1:], N)])
+    x, y = x0_h[0, 0].copy(), x0_h[0, 1].copy()
+    fx, fy = 0.0, float(cfg.foot_spread)
+    cur = spad[0]
+    side = "left"
+    t0 = time.perf_counter()
+    steps, err = 0, 0.0
+    for i in range(n - 1):
+        if time.perf_counter() - t0 > budget_s and steps >= 2:
+            break
+        # the GPU walk's own state and foot as input: each timed QP is checked one by one
+        x, y = hist_gpu[0, i, 0], hist_gpu[0, i, 1]
+        fx, fy = foot_gpu[0, i]
+        xn, yn, _, _ = HO.herdt_step(cfg, x, y, vpad[i + 1: i + 1 + N], fx, fy, cur,
+                                     spad[i + 1: i + 1 + N], side)
+        if i == n // 2:
+            yn = yn - np.array([0.0, kick_h[0], 0.0])
+        err = max(err, float(np.abs(xn - hist_gpu[0, i + 1, 0]).max()),
+                  float(np.abs(yn - hist_gpu[0, i + 1, 1]).max()))
+        if spad[i + 1] != cur and cur == 2:
+            side = "left" if side == "right" else "right"
+        if spad[i + 1] != cur:
+            cur = spad[i + 1]
+        steps += 1
+    el = time.perf_counter() - t0
+    return {"value": steps / el, "unit": "QP solves/s", "cores": cpu_share(), "kind": "port",
+            "sample": f"{steps} consecutive joint QPs of walk 0 (exact Goldfarb-Idnani NumPy "
+                      "port of predict_herdt_joint; the reference's cvxpy/OSQP is not "
+                      "installed), default BLAS threads",
+            "seconds": el, "max_abs_state_gpu_vs_port": err}
 
 
 def make_batch(B, rank, cfg, shared):
@@ -247,7 +404,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", type=int, default=2, choices=sorted(CONFIGS),
-                    help="SURVEY.md §8d workload (2 = BASELINE.json metric config)")
+                    help="SURVEY.md §8d workload (2 = BASELINE.json metric config; 6 = Herdt)")
     ap.add_argument("--batch", type=int, default=None, help="walks per GPU (config default)")
     ap.add_argument("--horizon", type=int, default=None)
     ap.add_argument("--strict", action="store_true", help="alias of --config 3")
@@ -271,6 +428,13 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
 
     conf = 3 if args.strict else args.config
+    if CONFIGS[conf].get("herdt"):
+        line = herdt_bench(args, rank, world, dev)
+        if rank == 0:
+            print(json.dumps(line))
+        if world > 1:
+            dist.destroy_process_group()
+        return
     wl = dict(CONFIGS[conf])
     if args.unconstrained:
         wl["strict"] = False
@@ -432,7 +596,7 @@ def main():
                     "working_set_slot_frac": ws / max(1, slots)}
         roof.update({
             "traffic": traffic,
-            "kernel": "zmpc_strict_lq_kernel" if cfg.strict else "zmpc_rollout_unc_kernel",
+            "kernel": rollout_kernel_name(B, n, cfg.horizon, cfg.strict),
             "kernel_ms": kern_ms, "alg_bytes_per_launch": alg_bytes,
             "hbm_gbs": achieved, "alg_flops_per_launch": flops,
             "fp64_frac_alg": flops / (kern_ms * 1e-3) / (FP64_PEAK_TFS * 1e12),

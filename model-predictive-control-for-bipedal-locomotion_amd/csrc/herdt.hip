@@ -299,11 +299,21 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
       for (int q = 0; q < NP; ++q) P[q] = 0.0;
 #pragma unroll
       for (int q = 0; q < NA; ++q) s[q] = 0.0;
+      // global loads are issued one row ahead of their use (at one wave per SIMD nothing else
+      // hides their latency)
+      double vr_next = vref(N - 1);
+      int sg_n = segb[(N - 1) * 64 + lane], kd_n = kind[(N - 1) * 64 + lane],
+          wk_n = wset[(N - 1) * 64 + lane];
       for (int k = N - 1; k >= 0; --k) {
-        const int sg = segb[k * 64 + lane];
-        const int kd = kind[k * 64 + lane];
-        const int wk = wset[k * 64 + lane];
-        const double vr = vref(k);
+        const int sg = sg_n, kd = kd_n, wk = wk_n;
+        const double vr = vr_next;
+        {
+          const int k1 = k > 0 ? k - 1 : 0;
+          vr_next = vref(k1);
+          sg_n = segb[k1 * 64 + lane];
+          kd_n = kind[k1 * 64 + lane];
+          wk_n = wset[k1 * 64 + lane];
+        }
         const int jf = sg - 1;  // footstep column of the ZMP centre (−1: current foot)
         const double fc0 = (sg == 0) ? fc : 0.0;
         // P B̂ (x part of B̂ only)
@@ -469,14 +479,27 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
       bool changed = false;
       {
         double xs[3] = {x[0], x[1], x[2]};
+        // row k's feedback (K, kff, Kf·f) and v_ref, loaded one row ahead
+        double nK0 = S(0, F_K), nK1 = S(0, F_K + 1), nK2 = S(0, F_K + 2), nkf = S(0, F_KFF);
+#pragma unroll
+        for (int q = 0; q < MM; ++q) nkf += S(0, F_KF + q) * fsol[q];
+        double nvr = vref(0);
         for (int k = 0; k < N; ++k) {
           const int sg = segb[k * 64 + lane];
           const int kd = kind[k * 64 + lane];
-          double fterm = S(k, F_KFF);
+          const double K0 = nK0, K1 = nK1, K2 = nK2, fterm = nkf, vrk = nvr;
+          {
+            const int k1 = k + 1 < N ? k + 1 : k;
+            nK0 = S(k1, F_K);
+            nK1 = S(k1, F_K + 1);
+            nK2 = S(k1, F_K + 2);
+            double t = S(k1, F_KFF);
 #pragma unroll
-          for (int q = 0; q < MM; ++q) fterm += S(k, F_KF + q) * fsol[q];
-          const double u = -(S(k, F_K) * xs[0] + S(k, F_K + 1) * xs[1] + S(k, F_K + 2) * xs[2]) -
-                           fterm;
+            for (int q = 0; q < MM; ++q) t += S(k1, F_KF + q) * fsol[q];
+            nkf = t;
+            nvr = vref(k1);
+          }
+          const double u = -(K0 * xs[0] + K1 * xs[1] + K2 * xs[2]) - fterm;
           if (k == 0) u0 = u;
           const double z = c1[0] * xs[0] + c1[1] * xs[1] + c1[2] * xs[2] + p0 * u;
           const double v = ev[1] * xs[1] + ev[2] * xs[2] + bv * u;
@@ -485,7 +508,7 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
           for (int q = 0; q < MM; ++q)
             if (sg - 1 == q) ccost = fsol[q];
           S(k, F_U) = u;
-          S(k, F_EV) = v - vref(k);
+          S(k, F_EV) = v - vrk;
           S(k, F_EZ) = z - ccost;
           const int wk = wset[k * 64 + lane];
           if (kd != CK_NONE && wk == 0) {
@@ -509,8 +532,15 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
       // ---- costate: multipliers of the pinned rows, dual check --------------------------------
       {
         double lam[3] = {0.0, 0.0, 0.0};
+        double nu_ = S(N - 1, F_U), nev = S(N - 1, F_EV), nez = S(N - 1, F_EZ);
         for (int k = N - 1; k >= 0; --k) {
-          const double u = S(k, F_U), e_v = S(k, F_EV), e_z = S(k, F_EZ);
+          const double u = nu_, e_v = nev, e_z = nez;
+          {
+            const int k1 = k > 0 ? k - 1 : 0;
+            nu_ = S(k1, F_U);
+            nev = S(k1, F_EV);
+            nez = S(k1, F_EZ);
+          }
           const int wk = wset[k * 64 + lane];
           const double bl = Bv[0] * lam[0] + Bv[1] * lam[1] + Bv[2] * lam[2];
           const double gu = al * u + be * bv * e_v + ga * p0 * e_z + bl;
@@ -636,7 +666,7 @@ hipError_t zmpc_launch_herdt(const zmpc_plan* p, const zmpc_herdt_params* prm, i
   a.foot = foot;
   a.status = status;
   const int mm = prm->max_footsteps;
-  const int MM = mm <= 2 ? 2 : mm <= 4 ? 4 : mm <= 6 ? 6 : mm <= 8 ? 8 : 0;
+  const int MM = mm <= 2 ? 2 : mm <= 4 ? 4 : mm <= 6 ? 6 : mm <= 7 ? 7 : mm <= 8 ? 8 : 0;
   if (MM == 0) {
     *why = "more than 8 footsteps inside one horizon window";
     return hipErrorInvalidValue;
@@ -664,6 +694,9 @@ hipError_t zmpc_launch_herdt(const zmpc_plan* p, const zmpc_herdt_params* prm, i
     case 6:
       hipLaunchKernelGGL(zmpc_herdt_kernel<6>, dim3((unsigned)blocks), dim3(64), lds, s, a);
       break;
+    case 7:
+      hipLaunchKernelGGL(zmpc_herdt_kernel<7>, dim3((unsigned)blocks), dim3(64), lds, s, a);
+      break;
     default:
       hipLaunchKernelGGL(zmpc_herdt_kernel<8>, dim3((unsigned)blocks), dim3(64), lds, s, a);
       break;
@@ -676,7 +709,8 @@ hipError_t zmpc_launch_herdt(const zmpc_plan* p, const zmpc_herdt_params* prm, i
 hipError_t zmpc_herdt_set_attrs() {
   hipError_t e = hipSuccess;
   const void* ks[] = {(const void*)zmpc_herdt_kernel<2>, (const void*)zmpc_herdt_kernel<4>,
-                      (const void*)zmpc_herdt_kernel<6>, (const void*)zmpc_herdt_kernel<8>};
+                      (const void*)zmpc_herdt_kernel<6>, (const void*)zmpc_herdt_kernel<7>,
+                      (const void*)zmpc_herdt_kernel<8>};
   for (const void* k : ks)
     if (e == hipSuccess)
       e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
