@@ -119,6 +119,8 @@ def herdt_bench(args, rank, world, dev):
     torch.cuda.synchronize()
     stream = torch.cuda.current_stream()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    plan.counters(reset=True)
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     ev0.record(stream)
     for _ in range(args.steps):
@@ -132,21 +134,18 @@ def herdt_bench(args, rank, world, dev):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     kern_ms = ev0.elapsed_time(ev1) / args.steps
+    cnt = plan.counters(reset=True)
     assert int(status.abs().max()) == 0, "solver reported a failed instance"
     solves_per_step = B * (n - 1) * world
     value = solves_per_step * args.steps / elapsed
-    # minimal algorithmic FP64 work of one joint QP: one backward Riccati pass over the
-    # augmented state (3 + m) and one forward + costate sweep, both axes, at the window's
-    # footstep count m (mean over the walk); 2·NA² + 14·NA + 40 FLOP per row and axis for the
-    # value-function update (NA = 3 + m), 60 for forward + costate
-    a, b = pad[:-1].astype(np.int64), pad[1:].astype(np.int64)
-    brk = ((a != b) & ~((a == 1) & (b == 2))).astype(np.int64)   # footstep breaks (herdt.py)
-    cs = np.concatenate([[0], np.cumsum(brk)])
-    m_win = cs[np.arange(n - 1) + N] - cs[np.arange(n - 1)]      # footsteps per window
-    na = 3.0 + m_win
-    per_row = 2 * na ** 2 + 14 * na + 40 + 60
-    flops = float(B * 2 * N * per_row.sum())
+    # algorithmic FP64 work per active-set pass, row and axis at the window's footstep count m
+    # (NA = 3 + m): 2·NA² + 14·NA + 40 FLOP for the value-function update, 60 for the forward
+    # and costate sweeps = 160 + 26 m + 2 m²; summed over the executed passes with the kernel's
+    # counters (zmpc_plan_counters [5..7]: passes, Σm, Σm²)
+    P, Sm, Sm2 = cnt["herdt_instance_passes"], cnt["herdt_footsteps"], cnt["herdt_footsteps_sq"]
+    flops = float(N * (160 * P + 26 * Sm + 2 * Sm2)) / args.steps
     tfs = flops / (kern_ms * 1e-3) / 1e12
+    passes_per_solve = P / (args.steps * 2 * B * (n - 1))
     if rank != 0:
         return None
     com_rmse_ref = None
@@ -176,8 +175,10 @@ def herdt_bench(args, rank, world, dev):
                      "frac": tfs / FP64_PEAK_TFS, "traffic": None,
                      "kernel": "zmpc_herdt_kernel", "kernel_ms": kern_ms,
                      "alg_flops_per_launch": flops,
-                     "engine": "FP64 VALU, one (walk, axis) per lane; the FLOP count is one "
-                               "active-set pass (a lower bound)"},
+                     "passes_per_solve": passes_per_solve,
+                     "wave_passes_per_launch": cnt["herdt_wave_passes"] / args.steps,
+                     "engine": "FP64 VALU, one (walk, axis) per lane; FLOPs = minimal per-row "
+                               "work x the executed active-set passes (kernel counters)"},
         "cpu_baseline": cpu, "com_rmse_vs_ref": com_rmse_ref}
 
 

@@ -74,19 +74,22 @@ int zmpc_plan_destroy(zmpc_plan* plan);
 int zmpc_plan_export(const zmpc_plan* plan, int32_t what, double* dst_host, int64_t count);
 
 /*
- * Work counters of a strict plan's box-QP solver, summed over its zmpc_step / zmpc_rollout
- * launches since creation or the last reset (diagnostics for the roofline accounting; the
- * reference has no equivalent).  Copied to HOST memory after synchronising the plan's device:
+ * Work counters of a plan's active-set solvers, summed over its launches since creation or the
+ * last reset (diagnostics for the roofline accounting; the reference has no equivalent).
+ * Copied to HOST memory after synchronising the plan's device.  Strict box-QP solver
+ * (zmpc_step / zmpc_rollout on a strict plan):
  *   [0] wave passes   (active-set passes of a 64-instance wave, lockstep)
  *   [1] instance passes (active-set iterations summed over instances and timesteps)
  *   [2] instance-slots through the working-set Riccati step (the rest of the
  *       [1] x N instance-slots took the free-tail step)
  *   [3] launches
+ * Herdt joint footstep QP (zmpc_herdt_rollout / zmpc_herdt_step, any plan; since ABI 4):
+ *   [4] wave passes, [5] instance passes (one instance = one walk axis),
+ *   [6] sum over instance passes of the window's footstep count m, [7] the same of m^2
  * count = number of uint64 dst can hold (at most ZMPC_NCOUNTERS are written); reset != 0
- * zeroes the counters after the copy.  A plan without strict workspace returns ZMPC_ESTATE.
- * Since ABI 3.
+ * zeroes the counters after the copy.  Since ABI 3 ([0..3]); [4..7] since ABI 4.
  */
-#define ZMPC_NCOUNTERS 4
+#define ZMPC_NCOUNTERS 8
 int zmpc_plan_counters(const zmpc_plan* plan, uint64_t* dst_host, int32_t count, int32_t reset);
 
 /*

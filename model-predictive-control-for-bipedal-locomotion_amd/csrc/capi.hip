@@ -140,12 +140,16 @@ int zmpc_plan_create(int device, int32_t N, double T, double T2_2, double T3_6, 
     }
     P->strict_slots = 2 * cus;
     if ((e = hipMalloc((void**)&P->lqtab, zmpc_strict_lq_table_doubles(N) * sizeof(double))) !=
-            hipSuccess ||
-        (e = hipMalloc((void**)&P->lqcnt, ZMPC_NCOUNTERS * sizeof(unsigned long long))) !=
-            hipSuccess) {
+        hipSuccess) {
       free_plan(P);
       return fail(ZMPC_ENOMEM, std::string("hipMalloc strict table: ") + hipGetErrorString(e));
     }
+  }
+  // work counters of the active-set solvers (strict and Herdt), every plan
+  if ((e = hipMalloc((void**)&P->lqcnt, ZMPC_NCOUNTERS * sizeof(unsigned long long))) !=
+      hipSuccess) {
+    free_plan(P);
+    return fail(ZMPC_ENOMEM, std::string("hipMalloc counters: ") + hipGetErrorString(e));
   }
   hipStream_t s = (hipStream_t)stream;
   (void)hipMemsetAsync(P->k, 0, ((size_t)P->Kpad + 64) * sizeof(double), s);
@@ -218,7 +222,7 @@ int zmpc_plan_counters(const zmpc_plan* P, uint64_t* dst, int32_t count, int32_t
   g_err.clear();
   if (!P || !dst) return fail(ZMPC_EINVAL, "NULL plan or destination");
   if (count < 0) return fail(ZMPC_EINVAL, "count < 0");
-  if (!P->lqcnt) return fail(ZMPC_ESTATE, "plan has no strict solver counters");
+  if (!P->lqcnt) return fail(ZMPC_ESTATE, "plan has no solver counters");
   DeviceGuard g(P->device);
   if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
   hipError_t e = hipDeviceSynchronize();

@@ -23,11 +23,19 @@
 // multipliers from a costate sweep, add violated rows, stop when the set repeats), warm-started
 // with the previous timestep's set shifted one row.
 //
+// A pass: sweep 1 runs the augmented Riccati (3 + the wave's footstep count) backward for V_0(x, f);
+// the footsteps follow; sweep 2 runs the 3-state Riccati with every ZMP centre now known (the
+// augmented control law at f = fsol) and keeps 4 doubles per row; the forward sweep rolls out,
+// checks the free rows' bounds and the pinned rows' multipliers (from sweep 2's value function,
+// no costate sweep).  Only sweep 2 writes and only the forward sweep reads per-row data.
+//
 // Mapping: one lane per (walk, axis), lanes 2w and 2w+1 = axes x, y of walk w; a one-wave
-// workgroup holds 32 walks.  Per-row feedback and forward values go through a per-wave global
-// slab ([row][field][64]); per-row segment index, constraint kind and working-set flag are LDS
-// bytes.
+// workgroup holds 32 walks.  Sweep 2's rows go through a per-wave global slab ([row][4][64]);
+// per-row segment index, constraint kind and working-set flag are LDS bytes, the swing
+// polygons (half-spaces and facet segments) LDS doubles.
 #include <cstdio>
+#include <cstdlib>
+#include <type_traits>
 
 #include "zmpc_internal.h"
 
@@ -69,10 +77,16 @@ struct HerdtArgs {
   int32_t* status;
   double* ws;            // per-wave slab [waves][N][NF][64]
   int nf;                // doubles per row in the slab
+  unsigned long long* cnt;  // plan work counters [4..7] (zmpc_plan_counters), may be null
+  unsigned long long* prof; // diagnostics (ZMPC_HERDT_PROF): clock per phase, summed; null
 };
 
-// Row fields of the slab: K (3), kff, u, ev (= v − vr), ez (= z − c), Kf (MM)
-constexpr int F_K = 0, F_KFF = 3, F_U = 4, F_EV = 5, F_EZ = 6, F_KF = 7;
+// Slab row k (4 doubles, written by sweep 2, read by the forward sweep):
+//   free row:   K (3), kff        — the control law u = −K x − kff at the solved footsteps
+//   pinned row: PB̂ (3), B̂ᵀs of V_{k+1} — the costate B̂ᵀλ_{k+1} = B̂ᵀ∇V_{k+1}(x_{k+1}) for the
+//               row's multiplier (its u is fixed by the row)
+constexpr int SLAB = 4;
+constexpr int RB = 8;  // forward sweep: rows whose slab loads are in flight together
 
 // packed symmetric index (a <= b)
 template <int NA>
@@ -80,51 +94,85 @@ __device__ __forceinline__ constexpr int sidx(int a, int b) {
   return a <= b ? a * NA - a * (a - 1) / 2 + (b - a) : b * NA - b * (b - 1) / 2 + (a - b);
 }
 
-// Exact minimiser of ½σx(dx − ux)² + ½σy(dy − uy)² over {d : a_i·d <= b_i}: the interior
-// point, else the best feasible point among the facet-line projections and the vertices.
-__device__ void polytope_qp(const double (*P)[3], int nfac, double sx, double sy, double ux,
+// Swing-foot polygons in LDS (per workgroup, both sides): the half-spaces a·d <= b and, per
+// facet, the feasible segment of its boundary line [e0, e1] (x0 = NaN: empty).
+struct PolyLds {
+  double h[2][ZMPC_HERDT_MAX_FACETS][3];
+  double seg[2][ZMPC_HERDT_MAX_FACETS][4];
+};
+
+// Facet i of side sd: clip its line {a·d = b} by the other half-spaces (one lane per facet).
+__device__ void polytope_segment(const double (*P)[3], int nfac, int i, double* out) {
+  const double ax = P[i][0], ay = P[i][1], b = P[i][2];
+  const double n2 = ax * ax + ay * ay;
+  const double px = ax * b / n2, py = ay * b / n2;  // foot of the line
+  const double dx = -ay, dy = ax;                   // along the line
+  double lo = -1e300, hi = 1e300;
+  bool ok = true;
+  for (int j = 0; j < nfac; ++j) {
+    if (j == i) continue;
+    const double ad = P[j][0] * dx + P[j][1] * dy;
+    const double rr = P[j][2] - (P[j][0] * px + P[j][1] * py);
+    if (fabs(ad) < 1e-14) {
+      ok = ok && rr >= -1e-12;
+    } else if (ad > 0) {
+      hi = fmin(hi, rr / ad);
+    } else {
+      lo = fmax(lo, rr / ad);
+    }
+  }
+  if (!ok || lo > hi || lo < -1e299 || hi > 1e299) {
+    out[0] = __builtin_nan("");
+    out[1] = out[2] = out[3] = 0.0;
+    return;
+  }
+  out[0] = px + lo * dx;
+  out[1] = py + lo * dy;
+  out[2] = px + hi * dx;
+  out[3] = py + hi * dy;
+}
+
+// Exact minimiser of ½σx(dx − ux)² + ½σy(dy − uy)² over the polygon {d : a_i·d <= b_i}: the
+// unconstrained point when feasible, else the best clamped projection onto a facet segment
+// (the optimum of a convex QP outside its minimiser lies on the boundary: inside a facet, or
+// at a vertex = a segment end).
+__device__ void polytope_qp(const PolyLds& L, int sd, int nfac, double sx, double sy, double ux,
                             double uy, double* dx, double* dy) {
   const double tol = 1e-12;
-  auto feasible = [&](double px, double py) {
-    for (int i = 0; i < nfac; ++i)
-      if (P[i][0] * px + P[i][1] * py > P[i][2] + tol) return false;
-    return true;
-  };
-  if (feasible(ux, uy)) {
+  bool inside = true;
+  for (int i = 0; i < nfac; ++i)
+    inside = inside && (L.h[sd][i][0] * ux + L.h[sd][i][1] * uy <= L.h[sd][i][2] + tol);
+  if (inside) {
     *dx = ux;
     *dy = uy;
     return;
   }
   double best = 1e300, bx = ux, by = uy;
-  auto consider = [&](double px, double py) {
-    if (!feasible(px, py)) return;
+  for (int i = 0; i < nfac; ++i) {
+    const double* e = L.seg[sd][i];
+    if (isnan(e[0])) continue;
+    const double wx = e[2] - e[0], wy = e[3] - e[1];
+    const double rx = e[0] - ux, ry = e[1] - uy;
+    const double den = sx * wx * wx + sy * wy * wy;
+    double t = den > 0.0 ? -(sx * rx * wx + sy * ry * wy) / den : 0.0;
+    t = fmin(fmax(t, 0.0), 1.0);
+    const double px = e[0] + t * wx, py = e[1] + t * wy;
     const double v = 0.5 * sx * (px - ux) * (px - ux) + 0.5 * sy * (py - uy) * (py - uy);
     if (v < best) {
       best = v;
       bx = px;
       by = py;
     }
-  };
-  for (int i = 0; i < nfac; ++i) {
-    const double ax = P[i][0], ay = P[i][1], b = P[i][2];
-    const double den = ax * ax / sx + ay * ay / sy;
-    const double t = (ax * ux + ay * uy - b) / den;
-    consider(ux - t * ax / sx, uy - t * ay / sy);
-    for (int j = i + 1; j < nfac; ++j) {
-      const double cx = P[j][0], cy = P[j][1], c = P[j][2];
-      const double det = ax * cy - ay * cx;
-      if (fabs(det) < 1e-14) continue;
-      consider((b * cy - ay * c) / det, (ax * c - b * cx) / det);
-    }
   }
   *dx = bx;
   *dy = by;
 }
 
-// In-place Cholesky solve of the M×M block F (packed, NA-indexed at offset 3) for rhs g (M).
+// Cholesky factor of the M×M footstep block F of P (packed, NA-indexed at offset 3): L lower,
+// the reciprocal pivots in id.  False when F is not positive definite.
 template <int NA, int MM>
-__device__ __forceinline__ bool small_chol_solve(const double* P, int M, double* g) {
-  double L[MM][MM];
+__device__ __forceinline__ bool small_chol(const double* P, int M, double (&L)[MM][MM],
+                                           double (&id)[MM]) {
 #pragma unroll
   for (int i = 0; i < MM; ++i)
 #pragma unroll
@@ -132,6 +180,7 @@ __device__ __forceinline__ bool small_chol_solve(const double* P, int M, double*
   bool ok = true;
 #pragma unroll
   for (int k = 0; k < MM; ++k) {
+    id[k] = 0.0;
     if (k < M) {
       double d = L[k][k];
 #pragma unroll
@@ -140,6 +189,7 @@ __device__ __forceinline__ bool small_chol_solve(const double* P, int M, double*
       ok = ok && d > 0.0;
       const double piv = sqrt(fmax(d, 1e-300));
       L[k][k] = piv;
+      id[k] = 1.0 / piv;
 #pragma unroll
       for (int i = 0; i < MM; ++i) {
         if (i > k && i < M) {
@@ -147,12 +197,18 @@ __device__ __forceinline__ bool small_chol_solve(const double* P, int M, double*
 #pragma unroll
           for (int q = 0; q < MM; ++q)
             if (q < k) v -= L[i][q] * L[k][q];
-          L[i][k] = v / piv;
+          L[i][k] = v * id[k];
         }
       }
     }
   }
-  // forward / backward substitution
+  return ok;
+}
+
+// Solve F g' = g in place with the factor of small_chol.
+template <int MM>
+__device__ __forceinline__ void small_chol_solve(const double (&L)[MM][MM], const double (&id)[MM],
+                                                 int M, double* g) {
 #pragma unroll
   for (int i = 0; i < MM; ++i) {
     if (i < M) {
@@ -160,7 +216,7 @@ __device__ __forceinline__ bool small_chol_solve(const double* P, int M, double*
 #pragma unroll
       for (int q = 0; q < MM; ++q)
         if (q < i) v -= L[i][q] * g[q];
-      g[i] = v / L[i][i];
+      g[i] = v * id[i];
     }
   }
 #pragma unroll
@@ -170,24 +226,159 @@ __device__ __forceinline__ bool small_chol_solve(const double* P, int M, double*
 #pragma unroll
       for (int q = 0; q < MM; ++q)
         if (q > i && q < M) v -= L[q][i] * g[q];
-      g[i] = v / L[i][i];
+      g[i] = v * id[i];
     }
   }
-  return ok;
 }
 
 enum : unsigned char { CK_NONE = 0, CK_FOOT = 1, CK_STAND = 2 };
 
+// Per-lane constants of a Riccati row (see the kernel).
+struct RowC {
+  double T, T2, T3, bv, p0, ip, al, be, ga, c12;  // ip = 1/p0
+  double bnd, shi, slo;  // ZMP bounds: foot rows ±bnd around the centre, standing [slo, shi]
+};
+
+// One backward Riccati row on V_{k+1}(ξ) = ½ξᵀPξ − sᵀξ → V_k, in place, ξ = [x; f] (NA − 3
+// footstep columns).  Row k's stage cost: ½α u² + ½β(e_vᵀx + b_v u − vr)² + ½γ(c1ᵀx + p0 u −
+// c)² with the ZMP centre c = fc0 (jf < 0) or the footstep f_jf; wk ≠ 0 pins the row's ZMP to
+// a bound (u = (t + ccon − c1ᵀx)/p0, ccon = the centre on a foot row).  Outputs the row's
+// control law u = −K ξ − kff (x part K[0..2]) and V_{k+1}'s (PB̂)_x, B̂ᵀs (the pinned row's
+// costate map, see the forward sweep).
+template <int NA>
+__device__ __forceinline__ void herdt_row(const RowC& c, double* P, double* s, double vr,
+                                          double fc0, int jf, int kd, int wk, double* pbx,
+                                          double& sbo, double* Kx, double& kffo) {
+  const double T = c.T, T2 = c.T2, p0 = c.p0, bv = c.bv;
+  const double al = c.al, be = c.be, ga = c.ga;
+  const double c1[3] = {1.0, T, c.c12};
+  const double ev[3] = {0.0, 1.0, T};
+  const double Bv[3] = {c.T3, T2, T};
+  // P B̂ (x part of B̂ only)
+  double pb[NA];
+#pragma unroll
+  for (int q = 0; q < NA; ++q)
+    pb[q] = P[sidx<NA>(q, 0)] * Bv[0] + P[sidx<NA>(q, 1)] * Bv[1] + P[sidx<NA>(q, 2)] * Bv[2];
+  const double bpb = Bv[0] * pb[0] + Bv[1] * pb[1] + Bv[2] * pb[2];
+  const double Huu = al + be * bv * bv + ga * p0 * p0 + bpb;
+  // H_uξ
+  double Hu[NA];
+  Hu[0] = pb[0] + be * bv * ev[0] + ga * p0 * c1[0];
+  Hu[1] = T * pb[0] + pb[1] + be * bv * ev[1] + ga * p0 * c1[1];
+  Hu[2] = T2 * pb[0] + T * pb[1] + pb[2] + be * bv * ev[2] + ga * p0 * c1[2];
+#pragma unroll
+  for (int q = 3; q < NA; ++q) Hu[q] = pb[q] + ((q - 3 == jf) ? -ga * p0 : 0.0);
+  // h_u, h_ξ
+  const double sb = Bv[0] * s[0] + Bv[1] * s[1] + Bv[2] * s[2];
+  const double hu = sb + be * bv * vr + ga * p0 * fc0;
+  double hx[NA];
+  hx[0] = s[0] + be * ev[0] * vr + ga * c1[0] * fc0;
+  hx[1] = T * s[0] + s[1] + be * ev[1] * vr + ga * c1[1] * fc0;
+  hx[2] = T2 * s[0] + T * s[1] + s[2] + be * ev[2] * vr + ga * c1[2] * fc0;
+#pragma unroll
+  for (int q = 3; q < NA; ++q) hx[q] = s[q];
+  // H_ξξ = ÂᵀPÂ + stage
+  constexpr int NP = NA * (NA + 1) / 2;
+  double H[NP];
+  {
+    // PA: columns 0..2 transformed by A, f columns unchanged
+    double PA[NA][3];
+#pragma unroll
+    for (int q = 0; q < NA; ++q) {
+      const double p0q = P[sidx<NA>(q, 0)], p1q = P[sidx<NA>(q, 1)], p2q = P[sidx<NA>(q, 2)];
+      PA[q][0] = p0q;
+      PA[q][1] = T * p0q + p1q;
+      PA[q][2] = T2 * p0q + T * p1q + p2q;
+    }
+#pragma unroll
+    for (int r = 0; r < NA; ++r)
+#pragma unroll
+      for (int cc = r; cc < NA; ++cc) {
+        double v;
+        if (r < 3 && cc < 3) {
+          // (Aᵀ (P A))[r][cc]
+          v = (r == 0) ? PA[0][cc]
+                       : (r == 1) ? T * PA[0][cc] + PA[1][cc]
+                                  : T2 * PA[0][cc] + T * PA[1][cc] + PA[2][cc];
+          v += be * ev[r] * ev[cc] + ga * c1[r] * c1[cc];
+        } else if (r < 3) {
+          // (Aᵀ P)[r][cc] for an f column cc
+          const double q0 = P[sidx<NA>(0, cc)], q1 = P[sidx<NA>(1, cc)],
+                       q2 = P[sidx<NA>(2, cc)];
+          v = (r == 0) ? q0 : (r == 1) ? T * q0 + q1 : T2 * q0 + T * q1 + q2;
+          if (cc - 3 == jf) v += -ga * c1[r];
+        } else {
+          v = P[sidx<NA>(r, cc)];
+          if (r - 3 == jf && cc - 3 == jf) v += ga;
+        }
+        H[sidx<NA>(r, cc)] = v;
+      }
+  }
+  // control law u = −K̂ ξ − kff
+  double Kh[NA], kff;
+  if (wk == 0) {
+    // 1/Huu: hardware reciprocal + two Newton steps (Huu ≥ α + βb_v² + γp0² > 0)
+    double iq = __builtin_amdgcn_rcp(Huu);
+    iq = fma(iq, fma(-Huu, iq, 1.0), iq);
+    iq = fma(iq, fma(-Huu, iq, 1.0), iq);
+#pragma unroll
+    for (int q = 0; q < NA; ++q) Kh[q] = Hu[q] * iq;
+    kff = -hu * iq;
+  } else {
+    // pinned: c1ᵀx + p0 u − ccon = t  (ccon: the foot centre on a foot row, 0 standing)
+    const bool foot = kd == CK_FOOT;
+    const double t = (kd == CK_STAND) ? (wk == 1 ? c.shi : c.slo) : (wk == 1 ? c.bnd : -c.bnd);
+    const double cc0 = foot ? fc0 : 0.0;
+    const double ip = c.ip;
+    Kh[0] = c1[0] * ip;
+    Kh[1] = c1[1] * ip;
+    Kh[2] = c1[2] * ip;
+#pragma unroll
+    for (int q = 3; q < NA; ++q) Kh[q] = (foot && q - 3 == jf) ? -ip : 0.0;
+    kff = -(t + cc0) * ip;
+  }
+  double D[NA];
+#pragma unroll
+  for (int q = 0; q < NA; ++q) D[q] = Huu * Kh[q] - Hu[q];
+  // V_k: P = H − Hu K̂ᵀ + K̂ Dᵀ (symmetric), s = h − hu K̂ − kff D
+#pragma unroll
+  for (int r = 0; r < NA; ++r)
+#pragma unroll
+    for (int cc = r; cc < NA; ++cc)
+      P[sidx<NA>(r, cc)] = H[sidx<NA>(r, cc)] - Hu[r] * Kh[cc] + Kh[r] * D[cc];
+#pragma unroll
+  for (int q = 0; q < NA; ++q) s[q] = hx[q] - hu * Kh[q] - kff * D[q];
+  pbx[0] = pb[0];
+  pbx[1] = pb[1];
+  pbx[2] = pb[2];
+  sbo = sb;
+  Kx[0] = Kh[0];
+  Kx[1] = Kh[1];
+  Kx[2] = Kh[2];
+  kffo = kff;
+}
+
 template <int MM>
 __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
-  constexpr int NA = 3 + MM;
-  constexpr int NP = NA * (NA + 1) / 2;
   extern __shared__ __attribute__((aligned(16))) unsigned char hsm[];
   const int lane = threadIdx.x;
   const int N = a.N;
   unsigned char* segb = hsm;              // [N][64] support segment of row k (0 = current foot)
   unsigned char* kind = hsm + N * 64;     // [N][64] constraint kind
   unsigned char* wset = hsm + 2 * N * 64; // [N][64] working set: 0 free, 1 upper, 2 lower
+  PolyLds& pl = *reinterpret_cast<PolyLds*>(hsm + ((3 * N * 64 + 15) & ~15));
+  {
+    // both sides' half-spaces and facet segments, once per workgroup
+    const int sd = lane >> 5, i = lane & 31;
+    const int nf = sd == 0 ? a.nfl : a.nfr;
+    if (i < ZMPC_HERDT_MAX_FACETS) {
+      for (int c = 0; c < 3; ++c) pl.h[sd][i][c] = a.poly[sd][i][c];
+      double e[4] = {__builtin_nan(""), 0.0, 0.0, 0.0};
+      if (i < nf) polytope_segment(a.poly[sd], nf, i, e);
+      for (int c = 0; c < 4; ++c) pl.seg[sd][i][c] = e[c];
+    }
+    __syncthreads();
+  }
   const int64_t w = (int64_t)blockIdx.x * 32 + (lane >> 1);
   const int axis = lane & 1;
   const bool valid = w < a.B;
@@ -198,8 +389,7 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
   const double T = a.T, T2 = a.T2, T3 = a.T3;
   const double c1[3] = {1.0, T, a.c1_2};
   const double ev[3] = {0.0, 1.0, T};
-  const double Bv[3] = {T3, T2, T};
-  const double p0 = a.p0, bv = T2;
+  const double p0 = a.p0, bv = T2, ip0 = 1.0 / a.p0;
   const double al = a.alpha, be = a.beta, ga = a.gamma;
   const double bnd = axis ? a.by : a.bx;
 
@@ -229,6 +419,9 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
   air = fc;
   for (int k = 0; k < N; ++k) wset[k * 64 + lane] = 0;
   int fq = 0;
+  unsigned long long n_wave_pass = 0, n_pass = 0, n_m = 0, n_m2 = 0;
+  unsigned long long pr_b = 0, pr_f = 0, pr_w = 0, pr_t0 = a.prof ? clock64() : 0;
+  unsigned long long pr_kw = 0, pr_ns = 0;
   const int64_t nsteps = a.window_mode ? 1 : a.n - 1;
   const int64_t kstep = (!a.window_mode && axis == 1 && a.kick) ? a.kick_step : -1;
   const double kv = (kstep >= 0 && valid) ? a.kick[wc] : 0.0;
@@ -256,6 +449,9 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
       kind[k * 64 + lane] = (sk == ZMPC_STANDING) ? CK_STAND : CK_FOOT;
     }
     const int m = nbreak;                                // footsteps in the horizon
+    int mw = valid ? m : 0;  // the wave's largest m (wave-uniform): sweep 1's column count
+    for (int o = 32; o > 0; o >>= 1) mw = max(mw, __shfl_xor(mw, o));
+    mw = __builtin_amdgcn_readfirstlane(mw);
     const int M = m - ((m > 0 && lastbreak == N - 1) ? 1 : 0);  // with rows in the horizon
     const bool stand_mode = (cur == ZMPC_STANDING || nstand == N) && nstand > 0;
     if (m > MM) fq |= ZMPC_ST_FACTOR;  // host sizes MM from the batch; never expected
@@ -279,8 +475,8 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
       kind[k * 64 + lane] = kd;
       if (kd == CK_NONE) wset[k * 64 + lane] = 0;
     }
-    const double(*poly)[3] = a.poly[side];
     const int nfac = side == 0 ? a.nfl : a.nfr;
+    const RowC rc{T, T2, T3, bv, p0, ip0, al, be, ga, a.c1_2, bnd, shi, slo};
     auto vref = [&](int k) -> double {
       if (a.window_mode) return a.vref[(wc * a.vs / 2 + k) * 2 + axis];
       int64_t t = i + 1 + k;
@@ -293,274 +489,228 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
     int it = 0;
     bool again = true;
     while (again) {
-      // ---- backward Riccati over ξ = [x; f] --------------------------------------------------
-      double P[NP], s[NA];
-#pragma unroll
-      for (int q = 0; q < NP; ++q) P[q] = 0.0;
-#pragma unroll
-      for (int q = 0; q < NA; ++q) s[q] = 0.0;
-      // global loads are issued one row ahead of their use (at one wave per SIMD nothing else
-      // hides their latency)
-      double vr_next = vref(N - 1);
-      int sg_n = segb[(N - 1) * 64 + lane], kd_n = kind[(N - 1) * 64 + lane],
-          wk_n = wset[(N - 1) * 64 + lane];
-      for (int k = N - 1; k >= 0; --k) {
-        const int sg = sg_n, kd = kd_n, wk = wk_n;
-        const double vr = vr_next;
-        {
-          const int k1 = k > 0 ? k - 1 : 0;
-          vr_next = vref(k1);
-          sg_n = segb[k1 * 64 + lane];
-          kd_n = kind[k1 * 64 + lane];
-          wk_n = wset[k1 * 64 + lane];
-        }
-        const int jf = sg - 1;  // footstep column of the ZMP centre (−1: current foot)
-        const double fc0 = (sg == 0) ? fc : 0.0;
-        // P B̂ (x part of B̂ only)
-        double pb[NA];
-#pragma unroll
-        for (int q = 0; q < NA; ++q)
-          pb[q] = P[sidx<NA>(q, 0)] * Bv[0] + P[sidx<NA>(q, 1)] * Bv[1] +
-                  P[sidx<NA>(q, 2)] * Bv[2];
-        const double bpb = Bv[0] * pb[0] + Bv[1] * pb[1] + Bv[2] * pb[2];
-        const double Huu = al + be * bv * bv + ga * p0 * p0 + bpb;
-        // H_uξ
-        double Hu[NA];
-        Hu[0] = pb[0] + be * bv * ev[0] + ga * p0 * c1[0];
-        Hu[1] = T * pb[0] + pb[1] + be * bv * ev[1] + ga * p0 * c1[1];
-        Hu[2] = T2 * pb[0] + T * pb[1] + pb[2] + be * bv * ev[2] + ga * p0 * c1[2];
-#pragma unroll
-        for (int q = 3; q < NA; ++q) Hu[q] = pb[q] + ((q - 3 == jf) ? -ga * p0 : 0.0);
-        // h_u, h_ξ
-        const double sb = Bv[0] * s[0] + Bv[1] * s[1] + Bv[2] * s[2];
-        const double hu = sb + be * bv * vr + ga * p0 * fc0;
-        double hx[NA];
-        hx[0] = s[0] + be * ev[0] * vr + ga * c1[0] * fc0;
-        hx[1] = T * s[0] + s[1] + be * ev[1] * vr + ga * c1[1] * fc0;
-        hx[2] = T2 * s[0] + T * s[1] + s[2] + be * ev[2] * vr + ga * c1[2] * fc0;
-#pragma unroll
-        for (int q = 3; q < NA; ++q) hx[q] = s[q];
-        // H_ξξ = ÂᵀPÂ + stage
-        double H[NP];
-        {
-          // PA: columns 0..2 transformed by A, f columns unchanged
-          double PA[NA][3];
-#pragma unroll
-          for (int q = 0; q < NA; ++q) {
-            const double p0q = P[sidx<NA>(q, 0)], p1q = P[sidx<NA>(q, 1)],
-                         p2q = P[sidx<NA>(q, 2)];
-            PA[q][0] = p0q;
-            PA[q][1] = T * p0q + p1q;
-            PA[q][2] = T2 * p0q + T * p1q + p2q;
-          }
-#pragma unroll
-          for (int r = 0; r < NA; ++r)
-#pragma unroll
-            for (int c = r; c < NA; ++c) {
-              double v;
-              if (r < 3 && c < 3) {
-                // (Aᵀ (P A))[r][c]
-                v = (r == 0) ? PA[0][c]
-                             : (r == 1) ? T * PA[0][c] + PA[1][c]
-                                        : T2 * PA[0][c] + T * PA[1][c] + PA[2][c];
-                v += be * ev[r] * ev[c] + ga * c1[r] * c1[c];
-              } else if (r < 3) {
-                // (Aᵀ P)[r][c] for an f column c
-                const double q0 = P[sidx<NA>(0, c)], q1 = P[sidx<NA>(1, c)],
-                             q2 = P[sidx<NA>(2, c)];
-                v = (r == 0) ? q0 : (r == 1) ? T * q0 + q1 : T2 * q0 + T * q1 + q2;
-                if (c - 3 == jf) v += -ga * c1[r];
-              } else {
-                v = P[sidx<NA>(r, c)];
-                if (r - 3 == jf && c - 3 == jf) v += ga;
-              }
-              H[sidx<NA>(r, c)] = v;
-            }
-        }
-        // control law u = −K̂ ξ − kff
-        double Kh[NA], kff;
-        if (wk == 0) {
-          const double iq = 1.0 / Huu;
-#pragma unroll
-          for (int q = 0; q < NA; ++q) Kh[q] = Hu[q] * iq;
-          kff = -hu * iq;
-        } else {
-          // pinned: c1ᵀx + p0 u − ccon = t  (ccon: the foot centre on a foot row, 0 standing)
-          const bool foot = kd == CK_FOOT;
-          const double t = (kd == CK_STAND) ? (wk == 1 ? shi : slo) : (wk == 1 ? bnd : -bnd);
-          const double cc0 = foot ? fc0 : 0.0;
-          const double ip = 1.0 / p0;
-          Kh[0] = c1[0] * ip;
-          Kh[1] = c1[1] * ip;
-          Kh[2] = c1[2] * ip;
-#pragma unroll
-          for (int q = 3; q < NA; ++q) Kh[q] = (foot && q - 3 == jf) ? -ip : 0.0;
-          kff = -(t + cc0) * ip;
-        }
-        double D[NA];
-#pragma unroll
-        for (int q = 0; q < NA; ++q) D[q] = Huu * Kh[q] - Hu[q];
-        // V_k: P = H − Hu K̂ᵀ + K̂ Dᵀ (symmetric), s = h − hu K̂ − kff D
-#pragma unroll
-        for (int r = 0; r < NA; ++r)
-#pragma unroll
-          for (int c = r; c < NA; ++c)
-            P[sidx<NA>(r, c)] = H[sidx<NA>(r, c)] - Hu[r] * Kh[c] + Kh[r] * D[c];
-#pragma unroll
-        for (int q = 0; q < NA; ++q) s[q] = hx[q] - hu * Kh[q] - kff * D[q];
-        S(k, F_K + 0) = Kh[0];
-        S(k, F_K + 1) = Kh[1];
-        S(k, F_K + 2) = Kh[2];
-        S(k, F_KFF) = kff;
-#pragma unroll
-        for (int q = 0; q < MM; ++q) S(k, F_KF + q) = Kh[3 + q];
-      }
-      // ---- footsteps: minimise V_0(x, f) over f, first footstep in the polytope (:771-783)
-      double g[MM > 0 ? MM : 1];
-#pragma unroll
-      for (int q = 0; q < MM; ++q)
-        g[q] = s[3 + q] -
-               (P[sidx<NA>(0, 3 + q)] * x[0] + P[sidx<NA>(1, 3 + q)] * x[1] +
-                P[sidx<NA>(2, 3 + q)] * x[2]);
-      double sig = 1.0, uu = fc;  // marginal of the first footstep: ½σ(f0 − uu)²
-      if (M > 0) {
-        double gf[MM > 0 ? MM : 1];
-#pragma unroll
-        for (int q = 0; q < MM; ++q) gf[q] = g[q];
-        if (!small_chol_solve<NA, MM>(P, M, gf)) fq |= ZMPC_ST_FACTOR;
-        double e0[MM > 0 ? MM : 1];
-#pragma unroll
-        for (int q = 0; q < MM; ++q) e0[q] = (q == 0) ? 1.0 : 0.0;
-        small_chol_solve<NA, MM>(P, M, e0);
-        sig = 1.0 / e0[0];  // 1 / (F⁻¹)₀₀
-        uu = gf[0];
-      }
+      const unsigned long long tp0 = a.prof ? clock64() : 0;
+      // ---- sweep 1: backward Riccati over ξ = [x; f] for V_0(x, f), then the footsteps -----
+      // Run at the wave's footstep count (NW = 3 + mw columns, wave-uniform): lanes with fewer
+      // footsteps carry zero columns, and no lane pays for the MM − mw columns nobody has.
       double fx0 = 0.0;
-      if (m > 0) {
-        // pair exchange: x lane = even, y lane = odd
-        const double sx = __shfl(sig, lane & ~1, 64), sy = __shfl(sig, lane | 1, 64);
-        const double ux = __shfl(uu, lane & ~1, 64), uy = __shfl(uu, lane | 1, 64);
-        const double fcx = __shfl(fc, lane & ~1, 64), fcy = __shfl(fc, lane | 1, 64);
-        double dx, dy;
-        polytope_qp(poly, nfac, sx, sy, ux - fcx, uy - fcy, &dx, &dy);
-        fx0 = axis ? fcy + dy : fcx + dx;
-      }
-      // remaining footsteps: F_rr f_r = g_r − F_r0 f0
+      unsigned long long tp1 = 0;
+      auto sweep1 = [&](auto na_tag) {
+        constexpr int NW = decltype(na_tag)::value;  // 3 + footstep columns
+        constexpr int MW = NW - 3;
+        constexpr int NPW = NW * (NW + 1) / 2;
+        double P[NPW], s[NW];
 #pragma unroll
-      for (int q = 0; q < MM; ++q) fsol[q] = 0.0;
-      if (M > 0) {
-        fsol[0] = fx0;
-        if (M > 1) {
-          // solve the (M−1)×(M−1) block by solving the full system with f0 fixed:
-          // F [f0; f_r] = [*; g_r]  →  f_r = F_rr⁻¹ (g_r − F_r0 f0), via a shifted copy
-          double Pr[NP];
+        for (int q = 0; q < NPW; ++q) P[q] = 0.0;
 #pragma unroll
-          for (int q = 0; q < NP; ++q) Pr[q] = 0.0;
-#pragma unroll
-          for (int r = 0; r < MM; ++r)
-#pragma unroll
-            for (int c = r; c < MM; ++c)
-              if (r + 1 < MM && c + 1 < MM)
-                Pr[sidx<NA>(3 + r, 3 + c)] = P[sidx<NA>(3 + r + 1, 3 + c + 1)];
-          double gr[MM > 0 ? MM : 1];
-#pragma unroll
-          for (int q = 0; q < MM; ++q)
-            gr[q] = (q + 1 < MM) ? g[q + 1] - P[sidx<NA>(3, 3 + q + 1)] * fx0 : 0.0;
-          small_chol_solve<NA, MM>(Pr, M - 1, gr);
-#pragma unroll
-          for (int q = 1; q < MM; ++q)
-            if (q < M) fsol[q] = gr[q - 1];
-        }
-      } else if (m > 0) {
-        fsol[0] = fx0;  // the only footstep lies past the horizon: nearest polytope point
-      }
-      f0 = fx0;
-      // ---- forward: roll out, primal check ---------------------------------------------------
-      bool changed = false;
-      {
-        double xs[3] = {x[0], x[1], x[2]};
-        // row k's feedback (K, kff, Kf·f) and v_ref, loaded one row ahead
-        double nK0 = S(0, F_K), nK1 = S(0, F_K + 1), nK2 = S(0, F_K + 2), nkf = S(0, F_KFF);
-#pragma unroll
-        for (int q = 0; q < MM; ++q) nkf += S(0, F_KF + q) * fsol[q];
-        double nvr = vref(0);
-        for (int k = 0; k < N; ++k) {
-          const int sg = segb[k * 64 + lane];
-          const int kd = kind[k * 64 + lane];
-          const double K0 = nK0, K1 = nK1, K2 = nK2, fterm = nkf, vrk = nvr;
-          {
-            const int k1 = k + 1 < N ? k + 1 : k;
-            nK0 = S(k1, F_K);
-            nK1 = S(k1, F_K + 1);
-            nK2 = S(k1, F_K + 2);
-            double t = S(k1, F_KFF);
-#pragma unroll
-            for (int q = 0; q < MM; ++q) t += S(k1, F_KF + q) * fsol[q];
-            nkf = t;
-            nvr = vref(k1);
-          }
-          const double u = -(K0 * xs[0] + K1 * xs[1] + K2 * xs[2]) - fterm;
-          if (k == 0) u0 = u;
-          const double z = c1[0] * xs[0] + c1[1] * xs[1] + c1[2] * xs[2] + p0 * u;
-          const double v = ev[1] * xs[1] + ev[2] * xs[2] + bv * u;
-          double ccost = fc;
-#pragma unroll
-          for (int q = 0; q < MM; ++q)
-            if (sg - 1 == q) ccost = fsol[q];
-          S(k, F_U) = u;
-          S(k, F_EV) = v - vrk;
-          S(k, F_EZ) = z - ccost;
-          const int wk = wset[k * 64 + lane];
-          if (kd != CK_NONE && wk == 0) {
-            const double tol = 1e-11;
-            const double zz = (kd == CK_FOOT) ? z - ccost : z;
-            const double hi = (kd == CK_FOOT) ? bnd : shi, lo = (kd == CK_FOOT) ? -bnd : slo;
-            const int nf = (zz > hi + tol) ? 1 : ((zz < lo - tol) ? 2 : 0);
-            if (nf) {
-              wset[k * 64 + lane] = (unsigned char)nf;
-              changed = true;
-            }
-          }
-          double y0 = xs[0] + T * xs[1] + T2 * xs[2] + T3 * u;
-          double y1 = xs[1] + T * xs[2] + T2 * u;
-          double y2 = xs[2] + T * u;
-          xs[0] = y0;
-          xs[1] = y1;
-          xs[2] = y2;
-        }
-      }
-      // ---- costate: multipliers of the pinned rows, dual check --------------------------------
-      {
-        double lam[3] = {0.0, 0.0, 0.0};
-        double nu_ = S(N - 1, F_U), nev = S(N - 1, F_EV), nez = S(N - 1, F_EZ);
+        for (int q = 0; q < NW; ++q) s[q] = 0.0;
+        // row inputs are loaded one row ahead of their use (at one wave per SIMD nothing else
+        // hides their latency)
+        double vr_next = vref(N - 1);
+        int sg_n = segb[(N - 1) * 64 + lane], kd_n = kind[(N - 1) * 64 + lane],
+            wk_n = wset[(N - 1) * 64 + lane];
         for (int k = N - 1; k >= 0; --k) {
-          const double u = nu_, e_v = nev, e_z = nez;
+          const int sg = sg_n, kd = kd_n, wk = wk_n;
+          const double vr = vr_next;
           {
             const int k1 = k > 0 ? k - 1 : 0;
-            nu_ = S(k1, F_U);
-            nev = S(k1, F_EV);
-            nez = S(k1, F_EZ);
+            vr_next = vref(k1);
+            sg_n = segb[k1 * 64 + lane];
+            kd_n = kind[k1 * 64 + lane];
+            wk_n = wset[k1 * 64 + lane];
           }
-          const int wk = wset[k * 64 + lane];
-          const double bl = Bv[0] * lam[0] + Bv[1] * lam[1] + Bv[2] * lam[2];
-          const double gu = al * u + be * bv * e_v + ga * p0 * e_z + bl;
-          double nu = 0.0;
-          if (wk != 0) {
-            nu = -gu / p0;  // ≥ 0 at an upper, ≤ 0 at a lower bound
-            const double tn = 1e-10 * (1.0 + fabs(gu / p0));
-            if ((wk == 1 && nu < -tn) || (wk == 2 && nu > tn)) {
-              wset[k * 64 + lane] = 0;
-              changed = true;
-            }
+          double pbx[3], sb, Kx[3], kff;
+          herdt_row<NW>(rc, P, s, vr, (sg == 0) ? fc : 0.0, sg - 1, kd, wk, pbx, sb, Kx, kff);
+        }
+        if (a.prof) tp1 = clock64();
+        // ---- footsteps: minimise V_0(x, f) over f, first footstep in the polytope (:771-783)
+        double g[MW > 0 ? MW : 1];
+#pragma unroll
+        for (int q = 0; q < MW; ++q)
+          g[q] = s[3 + q] - (P[sidx<NW>(0, 3 + q)] * x[0] + P[sidx<NW>(1, 3 + q)] * x[1] +
+                             P[sidx<NW>(2, 3 + q)] * x[2]);
+        double sig = 1.0, uu = fc;  // marginal of the first footstep: ½σ(f0 − uu)²
+        double gf[MW > 0 ? MW : 1], e0[MW > 0 ? MW : 1];  // F⁻¹g, F⁻¹e₀
+        if constexpr (MW > 0) {
+          if (M > 0) {
+          double L[MW][MW], id[MW];
+          if (!small_chol<NW, MW>(P, M, L, id)) fq |= ZMPC_ST_FACTOR;
+#pragma unroll
+          for (int q = 0; q < MW; ++q) {
+            gf[q] = g[q];
+            e0[q] = (q == 0) ? 1.0 : 0.0;
           }
-          const double l0 = lam[0], l1 = lam[1], l2 = lam[2];
-          const double e = ga * e_z + nu;
-          lam[0] = l0 + c1[0] * e;
-          lam[1] = T * l0 + l1 + be * ev[1] * e_v + c1[1] * e;
-          lam[2] = T2 * l0 + T * l1 + l2 + be * ev[2] * e_v + c1[2] * e;
+          small_chol_solve<MW>(L, id, M, gf);
+          small_chol_solve<MW>(L, id, M, e0);
+          sig = 1.0 / e0[0];  // 1 / (F⁻¹)₀₀
+          uu = gf[0];
+          }
+        }
+        if (m > 0) {
+          // pair exchange: x lane = even, y lane = odd
+          const double sx = __shfl(sig, lane & ~1, 64), sy = __shfl(sig, lane | 1, 64);
+          const double ux = __shfl(uu, lane & ~1, 64), uy = __shfl(uu, lane | 1, 64);
+          const double fcx = __shfl(fc, lane & ~1, 64), fcy = __shfl(fc, lane | 1, 64);
+          double dx, dy;
+          polytope_qp(pl, side, nfac, sx, sy, ux - fcx, uy - fcy, &dx, &dy);
+          fx0 = axis ? fcy + dy : fcx + dx;
+        }
+        // the other footsteps minimise V_0 with f0 fixed: the KKT point of F f − g = μ e₀ is
+        // f = F⁻¹g + μ F⁻¹e₀ with μ from f0 = fx0
+#pragma unroll
+        for (int q = 0; q < MM; ++q) fsol[q] = 0.0;
+        if (MW > 0 && M > 0) {
+          const double mu = (fx0 - gf[0]) / e0[0];
+#pragma unroll
+          for (int q = 1; q < MW; ++q)
+            if (q < M) fsol[q] = fma(mu, e0[q], gf[q]);
+        }
+        if (m > 0) fsol[0] = fx0;  // (M = 0: the only footstep lies past the horizon)
+      };
+      switch (mw) {
+        case 0: sweep1(std::integral_constant<int, 3>{}); break;
+        case 1: sweep1(std::integral_constant<int, (MM >= 1 ? 4 : 3)>{}); break;
+        case 2: sweep1(std::integral_constant<int, (MM >= 2 ? 5 : 3)>{}); break;
+        case 3: sweep1(std::integral_constant<int, (MM >= 3 ? 6 : 3)>{}); break;
+        case 4: sweep1(std::integral_constant<int, (MM >= 4 ? 7 : 3)>{}); break;
+        case 5: sweep1(std::integral_constant<int, (MM >= 5 ? 8 : 3)>{}); break;
+        case 6: sweep1(std::integral_constant<int, (MM >= 6 ? 9 : 3)>{}); break;
+        case 7: sweep1(std::integral_constant<int, (MM >= 7 ? 10 : 3)>{}); break;
+        default: sweep1(std::integral_constant<int, 3 + MM>{}); break;
+      }
+      f0 = fx0;
+      // ---- sweep 2: the 3-state Riccati with every ZMP centre known (c_k = fc or f_jf), whose
+      // control law is the augmented one at f = fsol; slab rows: 4 doubles ---------------------
+      {
+        double P3[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0}, s3[3] = {0.0, 0.0, 0.0};
+        double vr_nx = vref(N - 1);
+        int sg_nx = segb[(N - 1) * 64 + lane], kd_nx = kind[(N - 1) * 64 + lane],
+            wk_nx = wset[(N - 1) * 64 + lane];
+        for (int k = N - 1; k >= 0; --k) {
+          const int sg = sg_nx, kd = kd_nx, wk = wk_nx;
+          const double vr = vr_nx;
+          {
+            const int k1 = k > 0 ? k - 1 : 0;
+            vr_nx = vref(k1);
+            sg_nx = segb[k1 * 64 + lane];
+            kd_nx = kind[k1 * 64 + lane];
+            wk_nx = wset[k1 * 64 + lane];
+          }
+          double ck = fc;
+#pragma unroll
+          for (int q = 0; q < MM; ++q)
+            if (sg - 1 == q) ck = fsol[q];
+          double pbx[3], sb, Kx[3], kff;
+          herdt_row<3>(rc, P3, s3, vr, ck, -1, kd, wk, pbx, sb, Kx, kff);
+          // slab row: the control law of a free row, the costate map of a pinned one
+          const bool pin = wk != 0;
+          S(k, 0) = pin ? pbx[0] : Kx[0];
+          S(k, 1) = pin ? pbx[1] : Kx[1];
+          S(k, 2) = pin ? pbx[2] : Kx[2];
+          S(k, 3) = pin ? sb : kff;
         }
       }
+      // ---- forward: roll out, primal check of the free rows, dual check of the pinned rows --
+      // A pinned row's multiplier comes from the stationarity of its u:
+      //   ν_k p0 = −(α u + β b_v (v − vr) + γ p0 (z − c) + B̂ᵀλ_{k+1}),
+      //   λ_{k+1} = ∇_x V_{k+1}(x_{k+1}) = P x_{k+1} − s of sweep 2 at row k + 1,
+      // so B̂ᵀλ_{k+1} = (PB̂)·x_{k+1} − B̂ᵀs from the slab (the reference's KKT multiplier of
+      // that row; the same value a backward costate sweep accumulates).
+      // Slab rows are loaded RB at a time: at one wave per SIMD nothing else hides the
+      // latency of a row's loads.
+      bool changed = false;
+      const unsigned long long tp2 = a.prof ? clock64() : 0;
+      {
+        double xs[3] = {x[0], x[1], x[2]};
+        for (int k0 = 0; k0 < N; k0 += RB) {
+          // every load of the block is issued before the first use
+          double fk[RB][4], vrb[RB];
+          int sgb[RB], kdb[RB], wkb[RB];
+#pragma unroll
+          for (int r = 0; r < RB; ++r) {
+            const int k = min(k0 + r, N - 1);  // rows past N: loaded, never used
+            fk[r][0] = S(k, 0);
+            fk[r][1] = S(k, 1);
+            fk[r][2] = S(k, 2);
+            fk[r][3] = S(k, 3);
+            vrb[r] = vref(k);
+            sgb[r] = segb[k * 64 + lane];
+            kdb[r] = kind[k * 64 + lane];
+            wkb[r] = wset[k * 64 + lane];
+          }
+#pragma unroll
+          for (int r = 0; r < RB; ++r) {
+            const int k = k0 + r;
+            if (k < N) {
+              const int sg = sgb[r], kd = kdb[r], wk = wkb[r];
+              double ccost = fc;
+#pragma unroll
+              for (int q = 0; q < MM; ++q)
+                if (sg - 1 == q) ccost = fsol[q];
+              double u;
+              if (wk == 0) {
+                u = -(fk[r][0] * xs[0] + fk[r][1] * xs[1] + fk[r][2] * xs[2]) - fk[r][3];
+              } else {
+                // pinned: c1ᵀx + p0 u − ccon = t (ccon: the ZMP centre on a foot row)
+                const double t = (kd == CK_STAND) ? (wk == 1 ? shi : slo) : (wk == 1 ? bnd : -bnd);
+                const double ccon = (kd == CK_FOOT) ? ccost : 0.0;
+                u = (t + ccon - (c1[0] * xs[0] + c1[1] * xs[1] + c1[2] * xs[2])) * ip0;
+              }
+              if (k == 0) u0 = u;
+              const double z = c1[0] * xs[0] + c1[1] * xs[1] + c1[2] * xs[2] + p0 * u;
+              const double v = ev[1] * xs[1] + ev[2] * xs[2] + bv * u;
+              const double y0 = xs[0] + T * xs[1] + T2 * xs[2] + T3 * u;
+              const double y1 = xs[1] + T * xs[2] + T2 * u;
+              const double y2 = xs[2] + T * u;
+              xs[0] = y0;
+              xs[1] = y1;
+              xs[2] = y2;
+              if (wk == 0) {
+                if (kd != CK_NONE) {
+                  const double tol = 1e-11;
+                  const double zz = (kd == CK_FOOT) ? z - ccost : z;
+                  const double hi = (kd == CK_FOOT) ? bnd : shi, lo = (kd == CK_FOOT) ? -bnd : slo;
+                  const int nf = (zz > hi + tol) ? 1 : ((zz < lo - tol) ? 2 : 0);
+                  if (nf) {
+                    wset[k * 64 + lane] = (unsigned char)nf;
+                    changed = true;
+                  }
+                }
+              } else {
+                const double bl = fk[r][0] * y0 + fk[r][1] * y1 + fk[r][2] * y2 - fk[r][3];
+                const double gu = al * u + be * bv * (v - vrb[r]) + ga * p0 * (z - ccost) + bl;
+                const double nu = -gu * ip0;  // ≥ 0 at an upper, ≤ 0 at a lower bound
+                const double tn = 1e-10 * (1.0 + fabs(nu));
+                if ((wk == 1 && nu < -tn) || (wk == 2 && nu > tn)) {
+                  wset[k * 64 + lane] = 0;
+                  changed = true;
+                }
+              }
+            }
+          }
+        }
+      }
+      if (a.prof) {
+        int kl = -1;
+        for (int k = 0; k < N; ++k)
+          if (wset[k * 64 + lane] != 0) kl = k;
+        for (int o = 32; o > 0; o >>= 1) kl = max(kl, __shfl_xor(kl, o));
+        pr_kw += (unsigned long long)(kl + 1);
+        int nset = 0;
+        for (int k = 0; k < N; ++k) nset += wset[k * 64 + lane] != 0;
+        pr_ns += (unsigned long long)nset;
+        const unsigned long long tp3 = clock64();
+        pr_b += tp1 - tp0;
+        pr_f += tp2 - tp1;
+        pr_w += tp3 - tp2;
+      }
       ++it;
+      ++n_wave_pass;
+      if (valid) {
+        ++n_pass;
+        n_m += (unsigned)m;
+        n_m2 += (unsigned)(m * m);
+      }
       if (changed && it >= HMAXIT) {
         fq |= ZMPC_ST_MAXITER;
         changed = false;
@@ -616,6 +766,31 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
     const int other = __shfl(fq, lane ^ 1, 64);
     if (axis == 0) a.status[wc] = fq | other;
   }
+  if (a.prof) {
+    for (int o = 32; o > 0; o >>= 1) pr_ns += __shfl_xor(pr_ns, o);
+    if (lane == 0) {
+      atomicAdd(a.prof + 0, pr_b);
+      atomicAdd(a.prof + 1, pr_f);
+      atomicAdd(a.prof + 2, pr_w);
+      atomicAdd(a.prof + 3, clock64() - pr_t0);
+      atomicAdd(a.prof + 4, pr_kw);
+      atomicAdd(a.prof + 5, pr_ns);
+      atomicAdd(a.prof + 6, n_wave_pass);
+    }
+  }
+  if (a.cnt) {
+    for (int o = 32; o > 0; o >>= 1) {
+      n_pass += __shfl_xor(n_pass, o);
+      n_m += __shfl_xor(n_m, o);
+      n_m2 += __shfl_xor(n_m2, o);
+    }
+    if (lane == 0) {
+      atomicAdd(a.cnt + 4, n_wave_pass);
+      atomicAdd(a.cnt + 5, n_pass);
+      atomicAdd(a.cnt + 6, n_m);
+      atomicAdd(a.cnt + 7, n_m2);
+    }
+  }
 }
 
 }  // namespace
@@ -665,20 +840,29 @@ hipError_t zmpc_launch_herdt(const zmpc_plan* p, const zmpc_herdt_params* prm, i
   a.hist = hist;
   a.foot = foot;
   a.status = status;
+  a.cnt = p->lqcnt;
+  static unsigned long long* prof = [] {  // diagnostics only: per-phase clocks to stderr
+    unsigned long long* q = nullptr;
+    if (getenv("ZMPC_HERDT_PROF") && hipMalloc((void**)&q, 8 * sizeof(unsigned long long)) != hipSuccess)
+      q = nullptr;
+    return q;
+  }();
+  if (prof) (void)hipMemsetAsync(prof, 0, 8 * sizeof(unsigned long long), s);
+  a.prof = prof;
   const int mm = prm->max_footsteps;
   const int MM = mm <= 2 ? 2 : mm <= 4 ? 4 : mm <= 6 ? 6 : mm <= 7 ? 7 : mm <= 8 ? 8 : 0;
   if (MM == 0) {
     *why = "more than 8 footsteps inside one horizon window";
     return hipErrorInvalidValue;
   }
-  a.nf = F_KF + MM;
+  a.nf = SLAB;
   const int64_t blocks = (B + 31) / 32;
   const size_t slab = (size_t)blocks * a.N * a.nf * 64 * sizeof(double);
   if (hipMallocAsync((void**)&a.ws, slab, s) != hipSuccess) {
     (void)hipGetLastError();
     return hipErrorOutOfMemory;
   }
-  const size_t lds = (size_t)3 * a.N * 64;
+  const size_t lds = (((size_t)3 * a.N * 64 + 15) & ~(size_t)15) + sizeof(PolyLds);
   if (lds > 160 * 1024) {
     (void)hipFreeAsync(a.ws, s);
     *why = "horizon too long for the Herdt solver's LDS flags";
@@ -703,6 +887,16 @@ hipError_t zmpc_launch_herdt(const zmpc_plan* p, const zmpc_herdt_params* prm, i
   }
   hipError_t e = hipGetLastError();
   const hipError_t ef = hipFreeAsync(a.ws, s);
+  if (a.prof && e == hipSuccess) {
+    unsigned long long h[8];
+    (void)hipMemcpy(h, a.prof, sizeof(h), hipMemcpyDeviceToHost);
+    const double t = (double)(h[3] ? h[3] : 1), wp = (double)(h[6] ? h[6] : 1);
+    fprintf(stderr,
+            "herdt prof: backward %.3f footsteps %.3f forward %.3f (of %llu clocks/wave); "
+            "rows to the wave's last pinned row %.1f, pinned rows per lane %.2f (per pass)\n",
+            h[0] / t, h[1] / t, h[2] / t, h[3] / (unsigned long long)blocks, h[4] / wp,
+            h[5] / (wp * 64));
+  }
   return e != hipSuccess ? e : ef;
 }
 

@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ZMPC_LIB", os.path.join(_HERE, "libzmpc.so"))
 
 ABI_VERSION = 4  # include/zmpc.h ZMPC_ABI_VERSION this binding is written for
-NCOUNTERS = 4    # include/zmpc.h ZMPC_NCOUNTERS
+NCOUNTERS = 8    # include/zmpc.h ZMPC_NCOUNTERS
 HERDT_MAX_FACETS = 16  # include/zmpc.h ZMPC_HERDT_MAX_FACETS
 
 ZMPC_OK = 0

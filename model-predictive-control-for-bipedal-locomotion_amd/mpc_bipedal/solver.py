@@ -73,13 +73,16 @@ class Plan:
         return buf
 
     def counters(self, reset: bool = False) -> dict:
-        """Strict solver work counters (zmpc_plan_counters, include/zmpc.h), summed over this
-        plan's launches since creation or the last reset; synchronises the device."""
+        """Active-set solver work counters (zmpc_plan_counters, include/zmpc.h), summed over this
+        plan's launches since creation or the last reset; synchronises the device.  Strict
+        solver: wave_passes .. launches; Herdt solver: the herdt_* keys."""
         buf = (ctypes.c_uint64 * _native.NCOUNTERS)()
         rc = _native.load().zmpc_plan_counters(self._h, buf, _native.NCOUNTERS, int(reset))
         _native.check(rc, "zmpc_plan_counters")
         return {"wave_passes": int(buf[0]), "instance_passes": int(buf[1]),
-                "working_set_slots": int(buf[2]), "launches": int(buf[3])}
+                "working_set_slots": int(buf[2]), "launches": int(buf[3]),
+                "herdt_wave_passes": int(buf[4]), "herdt_instance_passes": int(buf[5]),
+                "herdt_footsteps": int(buf[6]), "herdt_footsteps_sq": int(buf[7])}
 
     # -- launches --------------------------------------------------------------------------
     def _dev(self):
