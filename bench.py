@@ -70,10 +70,12 @@ CONFIGS = {
 }
 
 
-def rollout_kernel_name(B, n, N, strict):
+def rollout_kernel_name(B, n, N, strict, shared=False):
     """Which kernel zmpc_rollout launches for this shape (csrc/rollout.hip launch rules)."""
     if strict:
         return "zmpc_strict_lq_kernel"
+    if shared and n - 1 <= 512 and 6 * n * 8 <= 64 * 1024:
+        return "zmpc_rollout_unc_split_kernel<CW, true> (+ zmpc_shared_f_kernel)"
     if n - 1 <= 512:
         slots = 8 * torch.cuda.get_device_properties(0).multi_processor_count
         return ("zmpc_rollout_unc_pers_kernel" if slots < B <= 3 * slots
@@ -499,6 +501,10 @@ def main():
     alg_bytes = 2 * (1 if wl["shared"] else B) * n * 2 * 8 + B * n * 6 * 8
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     flops = B * (n - 1) * 2 * (2 * cfg.horizon + 20)
+    if wl["shared"] and not cfg.strict:
+        # one CoP for every walk: the gain dot k·z_ref (2N FLOP) of a (timestep, axis) is the
+        # same for all walks and is evaluated once per launch; 20 FLOP per solve remain
+        flops = B * (n - 1) * 2 * 20 + (n - 1) * 2 * 2 * cfg.horizon
     workload = (f"config{conf}" + ("_unc" if conf == 4 and not cfg.strict else "") +
                 f"_n{cfg.horizon}_b{B}")
 
@@ -597,7 +603,7 @@ def main():
                     "working_set_slot_frac": ws / max(1, slots)}
         roof.update({
             "traffic": traffic,
-            "kernel": rollout_kernel_name(B, n, cfg.horizon, cfg.strict),
+            "kernel": rollout_kernel_name(B, n, cfg.horizon, cfg.strict, wl["shared"]),
             "kernel_ms": kern_ms, "alg_bytes_per_launch": alg_bytes,
             "hbm_gbs": achieved, "alg_flops_per_launch": flops,
             "fp64_frac_alg": flops / (kern_ms * 1e-3) / (FP64_PEAK_TFS * 1e12),

@@ -128,6 +128,8 @@ struct RolloutArgs {
   int dbg;
   int srows;  // history rows the split-axis kernels stage per copy-out round
   const int64_t* kick_steps;  // [B] per-walk kick steps (ragged walks), or null: kick_step
+  const double* fsh;  // shared CoP (bounds stride 0): f of both axes, [2][fstride], or null
+  int fstride;
 };
 
 // The kick step of walk b: per walk (ragged batches) or the launch-wide one.
@@ -661,7 +663,7 @@ __global__ void __launch_bounds__(128, 8) zmpc_rollout_unc_axis_kernel(RolloutAr
 // One walk of the split kernel (shared by the one-walk-per-workgroup and the persistent
 // launch).  The tables read on wave-uniform addresses come in as __restrict__ pointers so the
 // compiler keeps them on scalar loads even inside a loop that stores the history.
-template <int CW>
+template <int CW, bool SHF = false>
 __device__ __forceinline__ void split_walk(const RolloutArgs& a, int64_t b, double* smem,
                                            int* flag, const double* __restrict__ kg,
                                            const double* __restrict__ scanP,
@@ -670,37 +672,44 @@ __device__ __forceinline__ void split_walk(const RolloutArgs& a, int64_t b, doub
   using ZL = ZrLayout<CW>;
   const int tid = threadIdx.x, lane = tid & 63, axis = tid >> 6;
   const int n = a.n, nsteps = n - 1;
-  double* zr0 = smem;
-  double* zr1 = zr0 + a.lzp;
-  // ---- 1. loads ----------------------------------------------------------------------------
-  AxisBounds<CW> r;
-  axis_load<CW>(a, b, tid, r);
-  const double2 hl = reinterpret_cast<const double2*>(a.zmax + b * a.bstride)[n - 1];
-  const double2 ll = reinterpret_cast<const double2*>(a.zmin + b * a.bstride)[n - 1];
+  double f[CW];
   const double* xb = a.x0 + b * 6 + 3 * axis;
   const double xi[3] = {xb[0], xb[1], xb[2]};
   const double kk = (axis == 1 && a.kick != nullptr) ? a.kick[b] : 0.0;
-  // ---- 2. z_ref rows + window padding (zmp_controller.py:81-88) ----------------------------
+  if constexpr (SHF) {
+    // shared CoP: f of this lane's timesteps, computed once per launch (zmpc_shared_f_kernel)
+    const double* fp = a.fsh + axis * a.fstride + lane * CW;
 #pragma unroll
-  for (int u = 0; u < AxisBounds<CW>::PF2; ++u) {
-    const int t = u * 128 + tid;
-    if (t < n) {
-      zr0[ZL::idx(t)] = (r.hi[u].x + r.lo[u].x) / 2;
-      zr1[ZL::idx(t)] = (r.hi[u].y + r.lo[u].y) / 2;
+    for (int q = 0; q < CW; ++q) f[q] = fp[q];
+  } else {
+    double* zr0 = smem;
+    double* zr1 = zr0 + a.lzp;
+    // ---- 1. loads --------------------------------------------------------------------------
+    AxisBounds<CW> r;
+    axis_load<CW>(a, b, tid, r);
+    const double2 hl = reinterpret_cast<const double2*>(a.zmax + b * a.bstride)[n - 1];
+    const double2 ll = reinterpret_cast<const double2*>(a.zmin + b * a.bstride)[n - 1];
+    // ---- 2. z_ref rows + window padding (zmp_controller.py:81-88) --------------------------
+#pragma unroll
+    for (int u = 0; u < AxisBounds<CW>::PF2; ++u) {
+      const int t = u * 128 + tid;
+      if (t < n) {
+        zr0[ZL::idx(t)] = (r.hi[u].x + r.lo[u].x) / 2;
+        zr1[ZL::idx(t)] = (r.hi[u].y + r.lo[u].y) / 2;
+      }
     }
-  }
-  {
-    const double l0 = (hl.x + ll.x) / 2, l1 = (hl.y + ll.y) / 2;
-    for (int t = n + tid; t < a.lz; t += 128) {
-      zr0[ZL::idx(t)] = l0;
-      zr1[ZL::idx(t)] = l1;
+    {
+      const double l0 = (hl.x + ll.x) / 2, l1 = (hl.y + ll.y) / 2;
+      for (int t = n + tid; t < a.lz; t += 128) {
+        zr0[ZL::idx(t)] = l0;
+        zr1[ZL::idx(t)] = l1;
+      }
     }
+    __syncthreads();
+    // ---- 3. correlation (this wave's axis) -------------------------------------------------
+    axis_correlate<CW>(a, kg, axis ? zr1 : zr0, lane, f);  // k: wave-uniform scalar loads
+    __syncthreads();  // z_ref dead: the area becomes the history staging (n rows of 6)
   }
-  __syncthreads();
-  // ---- 3. correlation (this wave's axis) ---------------------------------------------------
-  double f[CW];
-  axis_correlate<CW>(a, kg, axis ? zr1 : zr0, lane, f);  // k: wave-uniform scalar loads
-  __syncthreads();  // z_ref dead: the area becomes the history staging (n rows of 6)
   // ---- 4. lane-chunk affine scan -----------------------------------------------------------
   const int64_t kick_step = (axis == 1) ? kick_step_of(a, b) : -1;
   const LipmConsts lc = a.lc;
@@ -798,17 +807,38 @@ __device__ __forceinline__ void split_walk(const RolloutArgs& a, int64_t b, doub
 }
 
 
-template <int CW>
+template <int CW, bool SHF = false>
 __global__ void __launch_bounds__(128, 4) zmpc_rollout_unc_split_kernel(RolloutArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   __shared__ int flag[2];
-  split_walk<CW>(a, blockIdx.x, smem, flag, a.k, a.scanP, a.kx, a.hist);
+  split_walk<CW, SHF>(a, blockIdx.x, smem, flag, a.k, a.scanP, a.kx, a.hist);
+}
+
+// Shared CoP (bounds stride 0, e.g. an F_ext sweep over one walk): z_ref, and so f, is the
+// same for every walk, so the correlation runs once per launch — one thread per (axis,
+// timestep), the taps in the per-walk kernels' order (fma chain from 0 over j = 0..kc−1) — and
+// the rollout kernel reads it instead (split_walk<CW, true>); histories equal the per-walk
+// kernels' to rounding (≈1e-15 relative: the compiler contracts the two kernels differently).
+__global__ void __launch_bounds__(256) zmpc_shared_f_kernel(const double* __restrict__ zmax,
+                                                            const double* __restrict__ zmin,
+                                                            int n, const double* __restrict__ k,
+                                                            int kc, double* fsh, int fstride) {
+  const int i = blockIdx.x * 256 + threadIdx.x;  // timestep
+  const int axis = blockIdx.y;
+  if (i >= fstride) return;
+  double acc = 0.0;
+  for (int j = 0; j < kc; ++j) {
+    const int t = min(i + 1 + j, n - 1);  // window padding with the last row (:81-88)
+    const double z = (zmax[2 * t + axis] + zmin[2 * t + axis]) / 2;
+    acc = fma(k[j], z, acc);
+  }
+  fsh[axis * fstride + i] = acc;
 }
 
 // Persistent form: grid = resident workgroups (occupancy × CUs), walks strided over it — the
 // workgroups drift out of phase after the first walk, so one's history stores overlap
 // another's correlation (config 2: 45 µs vs 50 µs one walk per workgroup).
-template <int CW>
+template <int CW, bool SHF = false>
 __global__ void __launch_bounds__(128, 4)
     zmpc_rollout_unc_pers_kernel(RolloutArgs a, const double* __restrict__ kg,
                                  const double* __restrict__ scanP,
@@ -816,7 +846,7 @@ __global__ void __launch_bounds__(128, 4)
   extern __shared__ __attribute__((aligned(16))) double smem[];
   __shared__ int flag[2];
   for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x) {
-    split_walk<CW>(a, b, smem, flag, kg, scanP, kxp, hist);
+    split_walk<CW, SHF>(a, b, smem, flag, kg, scanP, kxp, hist);
     __syncthreads();  // staging read out before the next walk's z_ref overwrites it
   }
 }
@@ -1280,6 +1310,13 @@ void launch_unc(const RolloutGeom& g, size_t lds, hipStream_t s, const RolloutAr
   const size_t lds_axis = lds - (size_t)a.kcp * sizeof(double);  // no staged gain row
   const size_t lds_split = std::max<size_t>(lds_axis, 6 * (size_t)a.n * sizeof(double));
   RolloutArgs b = a;
+  if (a.fsh != nullptr) {
+    // shared CoP, f precomputed: scan, replay and the history stores only
+    const size_t lds_h = 6 * (size_t)a.n * sizeof(double);
+    hipLaunchKernelGGL((zmpc_rollout_unc_split_kernel<CW, true>), dim3((unsigned)a.B), dim3(128),
+                       lds_h, s, a);
+    return;
+  }
   if (g.passes == 1 && (variant == 8 || variant == 6) && lds_split <= 64 * 1024) {
     int per_cu = 0;
     if (variant == 8 &&
@@ -1336,7 +1373,7 @@ hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, con
   }();
   RolloutArgs a{g.kc, g.kcp, g.lz,      g.lzp, (int)n,     B,   p->lc,
                 p->k, p->kx,  zmax,      zmin,  bstride,    x0,  kick,
-                kick_step,    hist, status, p->scanP, dbg, 0, kick_steps};
+                kick_step,    hist, status, p->scanP, dbg, 0, kick_steps, nullptr, 0};
   WideGeom wg;
   static const bool no_wide = getenv("ZMPC_ROLLOUT_NO_WIDE") != nullptr;  // A/B: chunk kernel
   if (g.passes > 1 && (no_wide || !wide_geom(p->N, n, &wg))) {
@@ -1368,6 +1405,20 @@ hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, con
     }
     return hipGetLastError();
   }
+  // shared CoP (bounds stride 0) with a single-pass geometry: f once per launch
+  static const bool no_shared_f = getenv("ZMPC_NO_SHARED_F") != nullptr;  // A/B only
+  double* fsh = nullptr;
+  if (bstride == 0 && !no_shared_f && 6 * (size_t)n * sizeof(double) <= 64 * 1024) {
+    a.fstride = ((64 * g.cw) + 63) & ~63;  // every lane's CW values, padded
+    hipError_t e = hipMallocAsync((void**)&fsh, 2 * (size_t)a.fstride * sizeof(double), s);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      return hipErrorOutOfMemory;
+    }
+    hipLaunchKernelGGL(zmpc_shared_f_kernel, dim3((unsigned)((a.fstride + 255) / 256), 2),
+                       dim3(256), 0, s, zmax, zmin, (int)n, p->k, g.kc, fsh, a.fstride);
+    a.fsh = fsh;
+  }
   switch (g.cw) {
 #define ZMPC_CW(C)               \
   case C:                        \
@@ -1376,9 +1427,15 @@ hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, con
     ZMPC_CW(1) ZMPC_CW(2) ZMPC_CW(3) ZMPC_CW(4) ZMPC_CW(5) ZMPC_CW(6) ZMPC_CW(7) ZMPC_CW(8)
 #undef ZMPC_CW
     default:
+      if (fsh) (void)hipFreeAsync(fsh, s);
       return hipErrorInvalidValue;
   }
-  return hipGetLastError();
+  hipError_t e = hipGetLastError();
+  if (fsh) {
+    const hipError_t ef = hipFreeAsync(fsh, s);
+    if (e == hipSuccess) e = ef;
+  }
+  return e;
 }
 
 hipError_t zmpc_launch_step_unc(const zmpc_plan* p, int64_t B, const double* x,
