@@ -70,12 +70,36 @@ CONFIGS = {
 }
 
 
+def fft_transform(n, N):
+    """Transform size P of the FFT correlation if zmpc_rollout takes it for this shape (the wide
+    kernel's rule in csrc/rollout.hip), else None."""
+    ns = n - 1
+    if ns <= 512 or ns > 4096:
+        return None
+    W = 2 if ns <= 1024 else (4 if ns <= 2048 else 8)
+    cw = -(-ns // (64 * W))
+    kc = -(-N // cw) * cw
+    lz = W * 64 * cw + kc + 1
+    lzp = ((lz + (1 if cw % 2 == 0 else 0) * (lz // cw) + 1) + 1) & ~1
+    if 2 * lzp * 8 > 64 * 1024:
+        return None
+    P = 256
+    while P < ns + N:
+        P *= 2
+    E = P // (128 * W) if P % (128 * W) == 0 else 0
+    if E not in (4, 8) or P > 8192 or P * 16 > 64 * 1024:
+        return None
+    return P
+
+
 def rollout_kernel_name(B, n, N, strict, shared=False):
     """Which kernel zmpc_rollout launches for this shape (csrc/rollout.hip launch rules)."""
     if strict:
         return "zmpc_strict_lq_kernel"
     if shared and n - 1 <= 512 and 6 * n * 8 <= 64 * 1024:
         return "zmpc_rollout_unc_split_kernel<CW, true> (+ zmpc_shared_f_kernel)"
+    if fft_transform(n, N):
+        return "zmpc_rollout_unc_wide_kernel<CW, W, E> (FFT correlation)"
     if n - 1 <= 512:
         slots = 8 * torch.cuda.get_device_properties(0).multi_processor_count
         return ("zmpc_rollout_unc_pers_kernel" if slots < B <= 3 * slots
@@ -505,6 +529,12 @@ def main():
         # one CoP for every walk: the gain dot k·z_ref (2N FLOP) of a (timestep, axis) is the
         # same for all walks and is evaluated once per launch; 20 FLOP per solve remain
         flops = B * (n - 1) * 2 * 20 + (n - 1) * 2 * 2 * cfg.horizon
+    direct_flops = B * (n - 1) * 2 * (2 * cfg.horizon + 20)
+    P_fft = None if cfg.strict else fft_transform(n, cfg.horizon)
+    if P_fft:
+        # FFT correlation (both axes in one complex signal): two P-point transforms
+        # (5 P log2 P real FLOP each, radix-2 count), the spectrum product (8 P), 20 per solve
+        flops = B * (2 * 5 * P_fft * int(np.log2(P_fft)) + 8 * P_fft + (n - 1) * 2 * 20)
     workload = (f"config{conf}" + ("_unc" if conf == 4 and not cfg.strict else "") +
                 f"_n{cfg.horizon}_b{B}")
 
@@ -608,6 +638,9 @@ def main():
             "hbm_gbs": achieved, "alg_flops_per_launch": flops,
             "fp64_frac_alg": flops / (kern_ms * 1e-3) / (FP64_PEAK_TFS * 1e12),
             "fp64_sustained_peak_tfs": FP64_SUSTAINED_TFS})
+        if P_fft:
+            roof.update({"fft_points": P_fft, "direct_form_flops_per_launch": direct_flops,
+                         "direct_form_equiv_tfs": direct_flops / (kern_ms * 1e-3) / 1e12})
         line = {
             "metric": "QP solves/sec (horizon=150, batched) at 1/2/4/8 MI355X; CoM RMSE vs ref",
             "value": value,

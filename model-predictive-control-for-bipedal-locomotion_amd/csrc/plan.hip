@@ -274,6 +274,39 @@ static hipError_t launch_gram_pu(const zmpc_plan* P, double diag, hipStream_t s)
   return hipGetLastError();
 }
 
+// FFT tables (rollout.hip, long walks): twiddles e^{−2πi m/PT}, m < PT (sincospi: the
+// argument −2m/PT is exact), and for every P = 2^p in [kFftPmin, PT] the gain spectrum
+// DFT(g)[q]/P, g[d] = k_{d−1} for d = 1..N (the correlation f_i = Σ_d g[d] z_{i+d}), summed
+// directly with exact table angles ((q·d) mod P).
+__global__ void zmpc_fft_twiddles(double* tw) {
+  const int m = blockIdx.x * 256 + threadIdx.x;
+  if (m >= kFftPT) return;
+  double sn, cs;
+  sincospi(-2.0 * (double)m / (double)kFftPT, &sn, &cs);
+  tw[2 * m] = cs;
+  tw[2 * m + 1] = sn;
+}
+
+__global__ void zmpc_fft_gain(int N, const double* __restrict__ k, const double* __restrict__ tw,
+                              double* g) {
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= kFftGComplex) return;
+  int P = kFftPmin;
+  while (idx >= 2 * P - kFftPmin) P *= 2;
+  const int q = idx - (P - kFftPmin);
+  const int sh = kFftPT / P;
+  double re = 0.0, im = 0.0;
+  int m = 0;  // (q·d) mod P
+  for (int d = 1; d <= N; ++d) {
+    m = (m + q) & (P - 1);
+    const double kd = k[d - 1];
+    re = fma(kd, tw[2 * (m * sh)], re);
+    im = fma(kd, tw[2 * (m * sh) + 1], im);
+  }
+  g[2 * idx] = re / P;
+  g[2 * idx + 1] = im / P;
+}
+
 hipError_t zmpc_launch_plan(zmpc_plan* P, hipStream_t s) {
   const int N = P->N;
   hipError_t e;
@@ -294,6 +327,13 @@ hipError_t zmpc_launch_plan(zmpc_plan* P, hipStream_t s) {
   hipLaunchKernelGGL(zmpc_scan_matrices, dim3(1), dim3(64), 0, s, P->T, P->T2_2, P->T3_6, P->kx,
                      P->scanP);
   if ((e = hipGetLastError()) != hipSuccess) return e;
+  if (P->fft_tw && P->fft_g) {
+    hipLaunchKernelGGL(zmpc_fft_twiddles, dim3(kFftPT / 256), dim3(256), 0, s, P->fft_tw);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL(zmpc_fft_gain, dim3((kFftGComplex + 255) / 256), dim3(256), 0, s, N, P->k,
+                       P->fft_tw, P->fft_g);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
   if (P->strict) {
     hipLaunchKernelGGL(zmpc_solve_LPuT, dim3((N + 63) / 64), dim3(64), 0, s, N, P->L, P->p,
                        P->X);

@@ -130,6 +130,8 @@ struct RolloutArgs {
   const int64_t* kick_steps;  // [B] per-walk kick steps (ragged walks), or null: kick_step
   const double* fsh;  // shared CoP (bounds stride 0): f of both axes, [2][fstride], or null
   int fstride;
+  const double2* fft_tw;  // plan twiddles e^{−2πi m/kFftPT} (FFT correlation, wide kernel)
+  const double2* fft_g;   // plan gain spectrum DFT(g)/P for this launch's P
 };
 
 // The kick step of walk b: per walk (ragged batches) or the launch-wide one.
@@ -851,12 +853,103 @@ __global__ void __launch_bounds__(128, 4)
   }
 }
 
+// ---- FFT correlation (long walks) ------------------------------------------------------------
+// f_i = Σ_{d=1..N} g[d] s[i+d] with g[d] = k_{d−1} and s = z_x + i z_y (both axes in one complex
+// signal; g is real, so Re and Im stay separate): a circular cross-correlation of period
+// P = 2^p ≥ n − 1 + N, so no output i ≤ n − 2 wraps.  Its spectrum is S·conj(DFT g); with
+// T = conj(S)·DFT(g)/P (the plan's fft_g) f = conj(DFT(T)): two forward transforms.  O(P log P)
+// instead of the direct form's N per output (N = 512: ≈10× fewer FP64 operations).
+// Stockham autosort, radix 4 (+ one radix-2 stage when p is odd), in place in LDS: each stage
+// reads all of its inputs, barrier, writes, barrier.  NT threads, E = P/NT points each.
+__device__ __forceinline__ double2 cmul(double2 a, double2 b) {
+  return make_double2(fma(a.x, b.x, -a.y * b.y), fma(a.x, b.y, a.y * b.x));
+}
+
+template <int NT, int E>
+__device__ __forceinline__ void fft_forward(double2* buf, const double2* __restrict__ tw, int tid) {
+  constexpr int P = NT * E;
+  constexpr int LOGP = __builtin_ctz(P);
+  constexpr int NR4 = LOGP / 2;
+  constexpr int B4 = E / 4;  // radix-4 butterflies per thread per stage
+  static_assert(E == 4 || E == 8, "FFT points per thread");
+#pragma unroll
+  for (int st = 0; st < NR4; ++st) {
+    const int Ns = 1 << (2 * st);
+    double2 y[B4][4];
+    int base[B4];
+#pragma unroll
+    for (int m = 0; m < B4; ++m) {
+      const int j = tid + NT * m;
+      const int kk = j & (Ns - 1);
+      double2 v0 = buf[j], v1 = buf[j + P / 4], v2 = buf[j + P / 2], v3 = buf[j + 3 * P / 4];
+      if (st > 0) {
+        const double2 w1 = tw[kk * (kFftPT / (4 * Ns))];
+        const double2 w2 = cmul(w1, w1), w3 = cmul(w2, w1);
+        v1 = cmul(v1, w1);
+        v2 = cmul(v2, w2);
+        v3 = cmul(v3, w3);
+      }
+      const double2 a0 = make_double2(v0.x + v2.x, v0.y + v2.y);
+      const double2 a1 = make_double2(v0.x - v2.x, v0.y - v2.y);
+      const double2 a2 = make_double2(v1.x + v3.x, v1.y + v3.y);
+      const double2 a3 = make_double2(v1.y - v3.y, v3.x - v1.x);  // (v1 − v3)·(−i)
+      y[m][0] = make_double2(a0.x + a2.x, a0.y + a2.y);
+      y[m][2] = make_double2(a0.x - a2.x, a0.y - a2.y);
+      y[m][1] = make_double2(a1.x + a3.x, a1.y + a3.y);
+      y[m][3] = make_double2(a1.x - a3.x, a1.y - a3.y);
+      base[m] = ((j - kk) << 2) + kk;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < B4; ++m)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) buf[base[m] + r * Ns] = y[m][r];
+    __syncthreads();
+  }
+  if constexpr (LOGP & 1) {
+    // last stage, radix 2 (Ns = P/2): j < P/2, k = j
+    constexpr int B2 = E / 2;
+    double2 y0[B2], y1[B2];
+#pragma unroll
+    for (int m = 0; m < B2; ++m) {
+      const int j = tid + NT * m;
+      const double2 v0 = buf[j];
+      const double2 v1 = cmul(buf[j + P / 2], tw[j * (kFftPT / P)]);
+      y0[m] = make_double2(v0.x + v1.x, v0.y + v1.y);
+      y1[m] = make_double2(v0.x - v1.x, v0.y - v1.y);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < B2; ++m) {
+      const int j = tid + NT * m;
+      buf[j] = y0[m];
+      buf[j + P / 2] = y1[m];
+    }
+    __syncthreads();
+  }
+}
+
+// buf holds s (P complex) → f = conj(DFT(conj(DFT s)·G)) in place (G = the plan's DFT(g)/P).
+template <int NT, int E>
+__device__ __forceinline__ void fft_correlate(double2* buf, const double2* __restrict__ tw,
+                                              const double2* __restrict__ G, int tid) {
+  fft_forward<NT, E>(buf, tw, tid);
+#pragma unroll
+  for (int m = 0; m < E; ++m) {
+    const int q = tid + NT * m;
+    const double2 S = buf[q], g = G[q];
+    buf[q] = make_double2(fma(S.x, g.x, S.y * g.y), fma(S.x, g.y, -S.y * g.x));  // conj(S)·g
+  }
+  __syncthreads();
+  fft_forward<NT, E>(buf, tw, tid);
+}
+
 // Long walks (64·8+1 < n ≤ 64·8·8+1): the split-axis structure widened to W waves per axis
 // (workgroup = 2·W waves; wave w of an axis owns timesteps [w·64·CW, (w+1)·64·CW)).  Each
 // wave scans its range from a zero state; the true start state of wave w is chained over the
 // waves' end states with M = (Ā^CW)^64 (plan level 6), and lane l adds (Ā^CW)^(l+1)·x_start by
 // binary powering.  History staged through the z_ref area in rounds (replay per round).
-template <int CW, int W>
+template <int CW, int W, int E = 0>
 __global__ void __launch_bounds__(128 * W, 4) zmpc_rollout_unc_wide_kernel(RolloutArgs a) {
   using ZL = ZrLayout<CW>;
   constexpr int NT = 128 * W;
@@ -870,7 +963,31 @@ __global__ void __launch_bounds__(128 * W, 4) zmpc_rollout_unc_wide_kernel(Rollo
   double* zr0 = smem;
   double* zr1 = zr0 + a.lzp;
   // ---- 1. z_ref rows + window padding (zmp_controller.py:81-88) ----------------------------
-  {
+  double f[CW];
+  const int mbeg = (w * 64 + lane) * CW;
+  if constexpr (E > 0) {
+    // FFT correlation: s[t] = (z_x, z_y) for t < P (rows past n − 1: the last row)
+    double2* buf = reinterpret_cast<double2*>(smem);
+    const double2* zmx = reinterpret_cast<const double2*>(a.zmax + b * a.bstride);
+    const double2* zmn = reinterpret_cast<const double2*>(a.zmin + b * a.bstride);
+    double2 hi[E], lo[E];
+#pragma unroll
+    for (int u = 0; u < E; ++u) {
+      const int tc = min(u * NT + tid, n - 1);
+      hi[u] = zmx[tc];
+      lo[u] = zmn[tc];
+    }
+#pragma unroll
+    for (int u = 0; u < E; ++u)
+      buf[u * NT + tid] = make_double2((hi[u].x + lo[u].x) / 2, (hi[u].y + lo[u].y) / 2);
+    __syncthreads();
+    fft_correlate<NT, E>(buf, a.fft_tw, a.fft_g, tid);
+#pragma unroll
+    for (int q = 0; q < CW; ++q) {
+      const double2 c = buf[min(mbeg + q, NT * E - 1)];
+      f[q] = axis ? -c.y : c.x;  // f = conj(DFT T): f_y = −Im
+    }
+  } else {
     const double2* zmx = reinterpret_cast<const double2*>(a.zmax + b * a.bstride);
     const double2* zmn = reinterpret_cast<const double2*>(a.zmin + b * a.bstride);
     for (int t0 = 0; t0 < a.lz; t0 += 4 * NT) {
@@ -890,15 +1007,13 @@ __global__ void __launch_bounds__(128 * W, 4) zmpc_rollout_unc_wide_kernel(Rollo
         }
       }
     }
+    __syncthreads();
+    // ---- 2. correlation ----------------------------------------------------------------------
+    axis_correlate<CW>(a, a.k, (axis ? zr1 : zr0) + ZL::idx(w * 64 * CW), lane, f);
   }
   const double* xb = a.x0 + b * 6 + 3 * axis;
   const double xi[3] = {xb[0], xb[1], xb[2]};
   const double kk = (axis == 1 && a.kick != nullptr) ? a.kick[b] : 0.0;
-  __syncthreads();
-  // ---- 2. correlation ------------------------------------------------------------------------
-  const int mbeg = (w * 64 + lane) * CW;
-  double f[CW];
-  axis_correlate<CW>(a, a.k, (axis ? zr1 : zr0) + ZL::idx(w * 64 * CW), lane, f);
   // ---- 3. scan: per-wave zero-start Kogge-Stone, then the cross-wave offsets ---------------
   const int64_t kick_step = (axis == 1) ? kick_step_of(a, b) : -1;
   const LipmConsts lc = a.lc;
@@ -1373,7 +1488,8 @@ hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, con
   }();
   RolloutArgs a{g.kc, g.kcp, g.lz,      g.lzp, (int)n,     B,   p->lc,
                 p->k, p->kx,  zmax,      zmin,  bstride,    x0,  kick,
-                kick_step,    hist, status, p->scanP, dbg, 0, kick_steps, nullptr, 0};
+                kick_step,    hist, status, p->scanP, dbg, 0, kick_steps, nullptr, 0,
+                nullptr,      nullptr};
   WideGeom wg;
   static const bool no_wide = getenv("ZMPC_ROLLOUT_NO_WIDE") != nullptr;  // A/B: chunk kernel
   if (g.passes > 1 && (no_wide || !wide_geom(p->N, n, &wg))) {
@@ -1389,12 +1505,32 @@ hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, con
     q.kc = wg.kc;
     q.lz = wg.lz;
     q.lzp = wg.lzp;
-    const size_t lds_w = 2 * (size_t)wg.lzp * sizeof(double);
+    size_t lds_w = 2 * (size_t)wg.lzp * sizeof(double);
+    // FFT correlation when the transform maps onto the workgroup (E = P/NT points per thread,
+    // 4 or 8) and fits the default LDS ceiling; ZMPC_NO_FFT keeps the direct form (A/B)
+    static const bool no_fft = getenv("ZMPC_NO_FFT") != nullptr;
+    int P = kFftPmin;
+    while (P < n - 1 + p->N) P *= 2;
+    const int NT = 128 * wg.w;
+    int E = (P % NT == 0) ? P / NT : 0;
+    if (no_fft || (E != 4 && E != 8) || P > kFftPT || (size_t)P * 16 > 64 * 1024) E = 0;
+    if (E) {
+      q.fft_tw = reinterpret_cast<const double2*>(p->fft_tw);
+      q.fft_g = reinterpret_cast<const double2*>(p->fft_g) + (P - kFftPmin);
+      lds_w = std::max(lds_w, (size_t)P * 16);
+    }
     switch (wg.w * 16 + wg.cw) {
-#define ZMPC_WCASE(W, C)                                                                      \
-  case W * 16 + C:                                                                            \
-    hipLaunchKernelGGL((zmpc_rollout_unc_wide_kernel<C, W>), dim3((unsigned)B), dim3(128 * W), \
-                       lds_w, s, q);                                                          \
+#define ZMPC_WCASE(W, C)                                                                         \
+  case W * 16 + C:                                                                               \
+    if (E == 4)                                                                                  \
+      hipLaunchKernelGGL((zmpc_rollout_unc_wide_kernel<C, W, 4>), dim3((unsigned)B),            \
+                         dim3(128 * W), lds_w, s, q);                                            \
+    else if (E == 8)                                                                             \
+      hipLaunchKernelGGL((zmpc_rollout_unc_wide_kernel<C, W, 8>), dim3((unsigned)B),            \
+                         dim3(128 * W), lds_w, s, q);                                            \
+    else                                                                                         \
+      hipLaunchKernelGGL((zmpc_rollout_unc_wide_kernel<C, W>), dim3((unsigned)B), dim3(128 * W), \
+                         lds_w, s, q);                                                           \
     break;
       ZMPC_WCASE(2, 5) ZMPC_WCASE(2, 6) ZMPC_WCASE(2, 7) ZMPC_WCASE(2, 8)
       ZMPC_WCASE(4, 5) ZMPC_WCASE(4, 6) ZMPC_WCASE(4, 7) ZMPC_WCASE(4, 8)

@@ -51,7 +51,16 @@ struct zmpc_plan {
   // strict LQ solver (strict_lq.hip): free-tail Riccati table [N][16] and work counters
   double* lqtab = nullptr;
   unsigned long long* lqcnt = nullptr;  // [ZMPC_NCOUNTERS]
+  // FFT correlation of long unconstrained walks (rollout.hip): twiddles e^{−2πi m/PT}
+  // [PT] complex, and per transform size P = 2^p in [kFftPmin, PT] the spectrum of the
+  // gain kernel g[d] = k_{d−1} (d = 1..N), DFT(g)/P, at complex offset P − kFftPmin
+  double* fft_tw = nullptr;
+  double* fft_g = nullptr;
 };
+
+constexpr int kFftPT = 8192;    // largest transform (twiddle table size)
+constexpr int kFftPmin = 256;   // smallest transform with a gain spectrum
+constexpr int kFftGComplex = 2 * kFftPT - kFftPmin;  // Σ_P P over P = kFftPmin..kFftPT
 
 // kernels launchers (plan.hip)
 hipError_t zmpc_launch_plan(zmpc_plan* p, hipStream_t s);
