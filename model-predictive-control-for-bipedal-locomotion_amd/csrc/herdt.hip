@@ -277,43 +277,6 @@ __device__ __forceinline__ void herdt_row(const RowC& c, double* P, double* s, d
   hx[2] = T2 * s[0] + T * s[1] + s[2] + be * ev[2] * vr + ga * c1[2] * fc0;
 #pragma unroll
   for (int q = 3; q < NA; ++q) hx[q] = s[q];
-  // H_ξξ = ÂᵀPÂ + stage
-  constexpr int NP = NA * (NA + 1) / 2;
-  double H[NP];
-  {
-    // PA: columns 0..2 transformed by A, f columns unchanged
-    double PA[NA][3];
-#pragma unroll
-    for (int q = 0; q < NA; ++q) {
-      const double p0q = P[sidx<NA>(q, 0)], p1q = P[sidx<NA>(q, 1)], p2q = P[sidx<NA>(q, 2)];
-      PA[q][0] = p0q;
-      PA[q][1] = T * p0q + p1q;
-      PA[q][2] = T2 * p0q + T * p1q + p2q;
-    }
-#pragma unroll
-    for (int r = 0; r < NA; ++r)
-#pragma unroll
-      for (int cc = r; cc < NA; ++cc) {
-        double v;
-        if (r < 3 && cc < 3) {
-          // (Aᵀ (P A))[r][cc]
-          v = (r == 0) ? PA[0][cc]
-                       : (r == 1) ? T * PA[0][cc] + PA[1][cc]
-                                  : T2 * PA[0][cc] + T * PA[1][cc] + PA[2][cc];
-          v += be * ev[r] * ev[cc] + ga * c1[r] * c1[cc];
-        } else if (r < 3) {
-          // (Aᵀ P)[r][cc] for an f column cc
-          const double q0 = P[sidx<NA>(0, cc)], q1 = P[sidx<NA>(1, cc)],
-                       q2 = P[sidx<NA>(2, cc)];
-          v = (r == 0) ? q0 : (r == 1) ? T * q0 + q1 : T2 * q0 + T * q1 + q2;
-          if (cc - 3 == jf) v += -ga * c1[r];
-        } else {
-          v = P[sidx<NA>(r, cc)];
-          if (r - 3 == jf && cc - 3 == jf) v += ga;
-        }
-        H[sidx<NA>(r, cc)] = v;
-      }
-  }
   // control law u = −K̂ ξ − kff
   double Kh[NA], kff;
   if (wk == 0) {
@@ -340,12 +303,49 @@ __device__ __forceinline__ void herdt_row(const RowC& c, double* P, double* s, d
   double D[NA];
 #pragma unroll
   for (int q = 0; q < NA; ++q) D[q] = Huu * Kh[q] - Hu[q];
-  // V_k: P = H − Hu K̂ᵀ + K̂ Dᵀ (symmetric), s = h − hu K̂ − kff D
+  // V_k: P = H − Hu K̂ᵀ + K̂ Dᵀ with H = ÂᵀPÂ + stage, updated in place block by block (each
+  // block reads only its own old entries, so H is never held whole)
+  {
+    // x-x block: AᵀP_xxA + stage
+    const double q00 = P[sidx<NA>(0, 0)], q01 = P[sidx<NA>(0, 1)], q02 = P[sidx<NA>(0, 2)];
+    const double q11 = P[sidx<NA>(1, 1)], q12 = P[sidx<NA>(1, 2)], q22 = P[sidx<NA>(2, 2)];
+    const double a01 = T * q00 + q01, a02 = T2 * q00 + T * q01 + q02;  // (P A) row 0, cols 1, 2
+    const double a11 = T * q01 + q11, a12 = T2 * q01 + T * q11 + q12;  // row 1
+    const double a21 = T * q02 + q12, a22 = T2 * q02 + T * q12 + q22;  // row 2
+    double Hx[3][3];
+    Hx[0][0] = q00;
+    Hx[0][1] = a01;
+    Hx[0][2] = a02;
+    Hx[1][1] = T * a01 + a11;
+    Hx[1][2] = T * a02 + a12;
+    Hx[2][2] = T2 * a02 + T * a12 + a22;
+    (void)a21;
 #pragma unroll
-  for (int r = 0; r < NA; ++r)
+    for (int r = 0; r < 3; ++r)
 #pragma unroll
-    for (int cc = r; cc < NA; ++cc)
-      P[sidx<NA>(r, cc)] = H[sidx<NA>(r, cc)] - Hu[r] * Kh[cc] + Kh[r] * D[cc];
+      for (int cc = r; cc < 3; ++cc) {
+        const double v = Hx[r][cc] + be * ev[r] * ev[cc] + ga * c1[r] * c1[cc];
+        P[sidx<NA>(r, cc)] = v - Hu[r] * Kh[cc] + Kh[r] * D[cc];
+      }
+  }
+#pragma unroll
+  for (int cc = 3; cc < NA; ++cc) {
+    // x-f column cc: (AᵀP)[r][cc] + stage
+    const double q0 = P[sidx<NA>(0, cc)], q1 = P[sidx<NA>(1, cc)], q2 = P[sidx<NA>(2, cc)];
+    const double cf = (cc - 3 == jf) ? -ga : 0.0;
+    const double h0 = q0 + cf * c1[0];
+    const double h1 = T * q0 + q1 + cf * c1[1];
+    const double h2 = T2 * q0 + T * q1 + q2 + cf * c1[2];
+    P[sidx<NA>(0, cc)] = h0 - Hu[0] * Kh[cc] + Kh[0] * D[cc];
+    P[sidx<NA>(1, cc)] = h1 - Hu[1] * Kh[cc] + Kh[1] * D[cc];
+    P[sidx<NA>(2, cc)] = h2 - Hu[2] * Kh[cc] + Kh[2] * D[cc];
+    // f-f column cc (rows 3..cc)
+#pragma unroll
+    for (int r = 3; r <= cc; ++r) {
+      const double v = P[sidx<NA>(r, cc)] + ((r - 3 == jf && cc - 3 == jf) ? ga : 0.0);
+      P[sidx<NA>(r, cc)] = v - Hu[r] * Kh[cc] + Kh[r] * D[cc];
+    }
+  }
 #pragma unroll
   for (int q = 0; q < NA; ++q) s[q] = hx[q] - hu * Kh[q] - kff * D[q];
   pbx[0] = pb[0];
