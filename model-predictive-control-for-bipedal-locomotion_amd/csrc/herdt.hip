@@ -358,6 +358,23 @@ __device__ __forceinline__ void herdt_row(const RowC& c, double* P, double* s, d
   kffo = kff;
 }
 
+// A free-tail row of sweep 2 (rows past the wave's last pinned row): P, K and 1/Huu are the
+// all-free recursion's (ktab: K0, K1, K2, 1/Huu), only s moves — herdt_row<3> of a free row
+// without the rounding residue D = Huu·K − Hu.
+__device__ __forceinline__ void herdt_tail_row(const RowC& c, double* s, double vr, double ck,
+                                               const double* kt, double& kffo) {
+  const double T = c.T, T2 = c.T2, p0 = c.p0, bv = c.bv, be = c.be, ga = c.ga;
+  const double sb = c.T3 * s[0] + T2 * s[1] + T * s[2];
+  const double hu = sb + be * bv * vr + ga * p0 * ck;
+  const double hx0 = s[0] + ga * ck;
+  const double hx1 = T * s[0] + s[1] + be * vr + ga * T * ck;
+  const double hx2 = T2 * s[0] + T * s[1] + s[2] + be * T * vr + ga * c.c12 * ck;
+  kffo = -hu * kt[3];
+  s[0] = hx0 - hu * kt[0];
+  s[1] = hx1 - hu * kt[1];
+  s[2] = hx2 - hu * kt[2];
+}
+
 template <int MM>
 __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char hsm[];
@@ -367,6 +384,11 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
   unsigned char* kind = hsm + N * 64;     // [N][64] constraint kind
   unsigned char* wset = hsm + 2 * N * 64; // [N][64] working set: 0 free, 1 upper, 2 lower
   PolyLds& pl = *reinterpret_cast<PolyLds*>(hsm + ((3 * N * 64 + 15) & ~15));
+  // free-tail feedback [N][3]: K of row k when rows k..N−1 are all free (it depends on the
+  // working set only; the bounds, v_ref and the centres enter kff)
+  double* ktab = reinterpret_cast<double*>(hsm + ((3 * N * 64 + 15) & ~15) + sizeof(PolyLds));
+  // (ktab row k: K0, K1, K2, 1/Huu; the all-free P after row k is in ptab, global, per
+  // workgroup: sweep 2 starts its full rows from it)
   {
     // both sides' half-spaces and facet segments, once per workgroup
     const int sd = lane >> 5, i = lane & 31;
@@ -383,7 +405,8 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
   const int axis = lane & 1;
   const bool valid = w < a.B;
   const int64_t wc = valid ? w : 0;  // clamped walk for loads (invalid lanes compute garbage)
-  double* slab = a.ws + (size_t)blockIdx.x * N * a.nf * 64;
+  double* slab = a.ws + (size_t)blockIdx.x * N * (a.nf * 64 + 6);
+  double* ptab = slab + (size_t)N * a.nf * 64;  // [N][6] all-free P (V_k), this workgroup
   auto S = [&](int k, int f) -> double& { return slab[((size_t)k * a.nf + f) * 64 + lane]; };
 
   const double T = a.T, T2 = a.T2, T3 = a.T3;
@@ -392,6 +415,31 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
   const double p0 = a.p0, bv = T2, ip0 = 1.0 / a.p0;
   const double al = a.alpha, be = a.beta, ga = a.gamma;
   const double bnd = axis ? a.by : a.bx;
+  {
+    // the free-tail table: sweep 2's recursion with every row free, from V_N = 0
+    const RowC rt{T, T2, T3, bv, p0, ip0, al, be, ga, a.c1_2, 0.0, 0.0, 0.0};
+    double Pt[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0}, st[3] = {0.0, 0.0, 0.0};
+    for (int k = N - 1; k >= 0; --k) {
+      double pbx[3], sb, Kx[3], kff;
+      // 1/Huu of the row as herdt_row computes it: Huu = α + βb_v² + γp0² + B̂ᵀPB̂ (old P)
+      const double pb0 = Pt[0] * T3 + Pt[1] * T2 + Pt[2] * T;
+      const double pb1 = Pt[1] * T3 + Pt[3] * T2 + Pt[4] * T;
+      const double pb2 = Pt[2] * T3 + Pt[4] * T2 + Pt[5] * T;
+      const double Huu = al + be * bv * bv + ga * p0 * p0 + (T3 * pb0 + T2 * pb1 + T * pb2);
+      double iq = __builtin_amdgcn_rcp(Huu);
+      iq = fma(iq, fma(-Huu, iq, 1.0), iq);
+      iq = fma(iq, fma(-Huu, iq, 1.0), iq);
+      herdt_row<3>(rt, Pt, st, 0.0, 0.0, -1, CK_NONE, 0, pbx, sb, Kx, kff);
+      if (lane == 0) {
+        ktab[k * 4 + 0] = Kx[0];
+        ktab[k * 4 + 1] = Kx[1];
+        ktab[k * 4 + 2] = Kx[2];
+        ktab[k * 4 + 3] = iq;
+        for (int q = 0; q < 6; ++q) ptab[k * 6 + q] = Pt[q];
+      }
+    }
+    __syncthreads();
+  }
 
   double x[3];
   const double* xp = a.x0 + (wc * 2 + axis) * 3;
@@ -495,6 +543,7 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
       // footsteps carry zero columns, and no lane pays for the MM − mw columns nobody has.
       double fx0 = 0.0;
       unsigned long long tp1 = 0;
+      int klane = -1;  // this lane's last pinned row (sweep 1 meets it first)
       auto sweep1 = [&](auto na_tag) {
         constexpr int NW = decltype(na_tag)::value;  // 3 + footstep columns
         constexpr int MW = NW - 3;
@@ -521,6 +570,7 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
           }
           double pbx[3], sb, Kx[3], kff;
           herdt_row<NW>(rc, P, s, vr, (sg == 0) ? fc : 0.0, sg - 1, kd, wk, pbx, sb, Kx, kff);
+          klane = (wk != 0 && klane < 0) ? k : klane;
         }
         if (a.prof) tp1 = clock64();
         // ---- footsteps: minimise V_0(x, f) over f, first footstep in the polytope (:771-783)
@@ -578,6 +628,11 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
         case 7: sweep1(std::integral_constant<int, (MM >= 7 ? 10 : 3)>{}); break;
         default: sweep1(std::integral_constant<int, 3 + MM>{}); break;
       }
+      // rows past the wave's last pinned row (the free tail) take K from ktab; the slab keeps
+      // only their kff
+      int kw = valid ? klane : -1;
+      for (int o = 32; o > 0; o >>= 1) kw = max(kw, __shfl_xor(kw, o));
+      kw = __builtin_amdgcn_readfirstlane(kw);
       f0 = fx0;
       // ---- sweep 2: the 3-state Riccati with every ZMP centre known (c_k = fc or f_jf), whose
       // control law is the augmented one at f = fsol; slab rows: 4 doubles ---------------------
@@ -586,7 +641,30 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
         double vr_nx = vref(N - 1);
         int sg_nx = segb[(N - 1) * 64 + lane], kd_nx = kind[(N - 1) * 64 + lane],
             wk_nx = wset[(N - 1) * 64 + lane];
-        for (int k = N - 1; k >= 0; --k) {
+        // free tail (rows past the wave's last pinned row): the s recursion with ktab's K, 1/Huu
+        for (int k = N - 1; k > kw; --k) {
+          const int sg = sg_nx;
+          const double vr = vr_nx;
+          {
+            const int k1 = k > 0 ? k - 1 : 0;
+            vr_nx = vref(k1);
+            sg_nx = segb[k1 * 64 + lane];
+            kd_nx = kind[k1 * 64 + lane];
+            wk_nx = wset[k1 * 64 + lane];
+          }
+          double ck = fc;
+#pragma unroll
+          for (int q = 0; q < MM; ++q)
+            if (sg - 1 == q) ck = fsol[q];
+          double kff;
+          herdt_tail_row(rc, s3, vr, ck, ktab + k * 4, kff);
+          S(k, 3) = kff;
+        }
+        if (kw >= 0 && kw + 1 < N) {
+#pragma unroll
+          for (int q = 0; q < 6; ++q) P3[q] = ptab[(kw + 1) * 6 + q];  // V_{kw+1}, all free
+        }
+        for (int k = kw; k >= 0; --k) {
           const int sg = sg_nx, kd = kd_nx, wk = wk_nx;
           const double vr = vr_nx;
           {
@@ -622,73 +700,89 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
       const unsigned long long tp2 = a.prof ? clock64() : 0;
       {
         double xs[3] = {x[0], x[1], x[2]};
-        for (int k0 = 0; k0 < N; k0 += RB) {
-          // every load of the block is issued before the first use
-          double fk[RB][4], vrb[RB];
-          int sgb[RB], kdb[RB], wkb[RB];
+        // rows [kb, ke) in blocks of RB; TAIL: K from ktab (rows past the wave's last pinned
+        // row), only kff from the slab
+        auto fwd = [&](auto tail_tag, int kb, int ke) {
+          constexpr bool TAIL = decltype(tail_tag)::value;
+          for (int k0 = kb; k0 < ke; k0 += RB) {
+            // every load of the block is issued before the first use
+            double fk[RB][4], vrb[RB];
+            int sgb[RB], kdb[RB], wkb[RB];
 #pragma unroll
-          for (int r = 0; r < RB; ++r) {
-            const int k = min(k0 + r, N - 1);  // rows past N: loaded, never used
-            fk[r][0] = S(k, 0);
-            fk[r][1] = S(k, 1);
-            fk[r][2] = S(k, 2);
-            fk[r][3] = S(k, 3);
-            vrb[r] = vref(k);
-            sgb[r] = segb[k * 64 + lane];
-            kdb[r] = kind[k * 64 + lane];
-            wkb[r] = wset[k * 64 + lane];
-          }
-#pragma unroll
-          for (int r = 0; r < RB; ++r) {
-            const int k = k0 + r;
-            if (k < N) {
-              const int sg = sgb[r], kd = kdb[r], wk = wkb[r];
-              double ccost = fc;
-#pragma unroll
-              for (int q = 0; q < MM; ++q)
-                if (sg - 1 == q) ccost = fsol[q];
-              double u;
-              if (wk == 0) {
-                u = -(fk[r][0] * xs[0] + fk[r][1] * xs[1] + fk[r][2] * xs[2]) - fk[r][3];
+            for (int r = 0; r < RB; ++r) {
+              const int k = min(k0 + r, ke - 1);  // rows past ke: loaded, never used
+              if (TAIL) {
+                fk[r][0] = ktab[k * 4 + 0];
+                fk[r][1] = ktab[k * 4 + 1];
+                fk[r][2] = ktab[k * 4 + 2];
               } else {
-                // pinned: c1ᵀx + p0 u − ccon = t (ccon: the ZMP centre on a foot row)
-                const double t = (kd == CK_STAND) ? (wk == 1 ? shi : slo) : (wk == 1 ? bnd : -bnd);
-                const double ccon = (kd == CK_FOOT) ? ccost : 0.0;
-                u = (t + ccon - (c1[0] * xs[0] + c1[1] * xs[1] + c1[2] * xs[2])) * ip0;
+                fk[r][0] = S(k, 0);
+                fk[r][1] = S(k, 1);
+                fk[r][2] = S(k, 2);
               }
-              if (k == 0) u0 = u;
-              const double z = c1[0] * xs[0] + c1[1] * xs[1] + c1[2] * xs[2] + p0 * u;
-              const double v = ev[1] * xs[1] + ev[2] * xs[2] + bv * u;
-              const double y0 = xs[0] + T * xs[1] + T2 * xs[2] + T3 * u;
-              const double y1 = xs[1] + T * xs[2] + T2 * u;
-              const double y2 = xs[2] + T * u;
-              xs[0] = y0;
-              xs[1] = y1;
-              xs[2] = y2;
-              if (wk == 0) {
-                if (kd != CK_NONE) {
-                  const double tol = 1e-11;
-                  const double zz = (kd == CK_FOOT) ? z - ccost : z;
-                  const double hi = (kd == CK_FOOT) ? bnd : shi, lo = (kd == CK_FOOT) ? -bnd : slo;
-                  const int nf = (zz > hi + tol) ? 1 : ((zz < lo - tol) ? 2 : 0);
-                  if (nf) {
-                    wset[k * 64 + lane] = (unsigned char)nf;
+              fk[r][3] = S(k, 3);
+              vrb[r] = vref(k);
+              sgb[r] = segb[k * 64 + lane];
+              kdb[r] = kind[k * 64 + lane];
+              wkb[r] = TAIL ? 0 : wset[k * 64 + lane];
+            }
+#pragma unroll
+            for (int r = 0; r < RB; ++r) {
+              const int k = k0 + r;
+              if (k < ke) {
+                const int sg = sgb[r], kd = kdb[r], wk = wkb[r];
+                double ccost = fc;
+#pragma unroll
+                for (int q = 0; q < MM; ++q)
+                  if (sg - 1 == q) ccost = fsol[q];
+                double u;
+                if (wk == 0) {
+                  u = -(fk[r][0] * xs[0] + fk[r][1] * xs[1] + fk[r][2] * xs[2]) - fk[r][3];
+                } else {
+                  // pinned: c1ᵀx + p0 u − ccon = t (ccon: the ZMP centre on a foot row)
+                  const double t =
+                      (kd == CK_STAND) ? (wk == 1 ? shi : slo) : (wk == 1 ? bnd : -bnd);
+                  const double ccon = (kd == CK_FOOT) ? ccost : 0.0;
+                  u = (t + ccon - (c1[0] * xs[0] + c1[1] * xs[1] + c1[2] * xs[2])) * ip0;
+                }
+                if (k == 0) u0 = u;
+                const double z = c1[0] * xs[0] + c1[1] * xs[1] + c1[2] * xs[2] + p0 * u;
+                const double v = ev[1] * xs[1] + ev[2] * xs[2] + bv * u;
+                const double y0 = xs[0] + T * xs[1] + T2 * xs[2] + T3 * u;
+                const double y1 = xs[1] + T * xs[2] + T2 * u;
+                const double y2 = xs[2] + T * u;
+                xs[0] = y0;
+                xs[1] = y1;
+                xs[2] = y2;
+                if (wk == 0) {
+                  if (kd != CK_NONE) {
+                    const double tol = 1e-11;
+                    const double zz = (kd == CK_FOOT) ? z - ccost : z;
+                    const double hi = (kd == CK_FOOT) ? bnd : shi,
+                                 lo = (kd == CK_FOOT) ? -bnd : slo;
+                    const int nf = (zz > hi + tol) ? 1 : ((zz < lo - tol) ? 2 : 0);
+                    if (nf) {
+                      wset[k * 64 + lane] = (unsigned char)nf;
+                      changed = true;
+                    }
+                  }
+                } else {
+                  const double bl = fk[r][0] * y0 + fk[r][1] * y1 + fk[r][2] * y2 - fk[r][3];
+                  const double gu =
+                      al * u + be * bv * (v - vrb[r]) + ga * p0 * (z - ccost) + bl;
+                  const double nu = -gu * ip0;  // ≥ 0 at an upper, ≤ 0 at a lower bound
+                  const double tn = 1e-10 * (1.0 + fabs(nu));
+                  if ((wk == 1 && nu < -tn) || (wk == 2 && nu > tn)) {
+                    wset[k * 64 + lane] = 0;
                     changed = true;
                   }
-                }
-              } else {
-                const double bl = fk[r][0] * y0 + fk[r][1] * y1 + fk[r][2] * y2 - fk[r][3];
-                const double gu = al * u + be * bv * (v - vrb[r]) + ga * p0 * (z - ccost) + bl;
-                const double nu = -gu * ip0;  // ≥ 0 at an upper, ≤ 0 at a lower bound
-                const double tn = 1e-10 * (1.0 + fabs(nu));
-                if ((wk == 1 && nu < -tn) || (wk == 2 && nu > tn)) {
-                  wset[k * 64 + lane] = 0;
-                  changed = true;
                 }
               }
             }
           }
-        }
+        };
+        fwd(std::false_type{}, 0, kw + 1);
+        fwd(std::true_type{}, kw + 1, N);
       }
       if (a.prof) {
         int kl = -1;
@@ -857,12 +951,13 @@ hipError_t zmpc_launch_herdt(const zmpc_plan* p, const zmpc_herdt_params* prm, i
   }
   a.nf = SLAB;
   const int64_t blocks = (B + 31) / 32;
-  const size_t slab = (size_t)blocks * a.N * a.nf * 64 * sizeof(double);
+  const size_t slab = (size_t)blocks * a.N * (a.nf * 64 + 6) * sizeof(double);
   if (hipMallocAsync((void**)&a.ws, slab, s) != hipSuccess) {
     (void)hipGetLastError();
     return hipErrorOutOfMemory;
   }
-  const size_t lds = (((size_t)3 * a.N * 64 + 15) & ~(size_t)15) + sizeof(PolyLds);
+  const size_t lds = (((size_t)3 * a.N * 64 + 15) & ~(size_t)15) + sizeof(PolyLds) +
+                     (size_t)a.N * 4 * sizeof(double);
   if (lds > 160 * 1024) {
     (void)hipFreeAsync(a.ws, s);
     *why = "horizon too long for the Herdt solver's LDS flags";
