@@ -865,83 +865,148 @@ __device__ __forceinline__ double2 cmul(double2 a, double2 b) {
   return make_double2(fma(a.x, b.x, -a.y * b.y), fma(a.x, b.y, a.y * b.x));
 }
 
-template <int NT, int E>
-__device__ __forceinline__ void fft_forward(double2* buf, const double2* __restrict__ tw, int tid) {
-  constexpr int P = NT * E;
-  constexpr int LOGP = __builtin_ctz(P);
-  constexpr int NR4 = LOGP / 2;
-  constexpr int B4 = E / 4;  // radix-4 butterflies per thread per stage
-  static_assert(E == 4 || E == 8, "FFT points per thread");
+// 8-point DFT in registers, forward sign (e^{−2πi/8} = (1 − i)/√2).
+__device__ __forceinline__ void dft8(double2 (&v)[8]) {
+  constexpr double h = 0.70710678118654752440;  // 1/√2
+  double2 a[4], c[4];
 #pragma unroll
-  for (int st = 0; st < NR4; ++st) {
-    const int Ns = 1 << (2 * st);
-    double2 y[B4][4];
-    int base[B4];
-#pragma unroll
-    for (int m = 0; m < B4; ++m) {
-      const int j = tid + NT * m;
-      const int kk = j & (Ns - 1);
-      double2 v0 = buf[j], v1 = buf[j + P / 4], v2 = buf[j + P / 2], v3 = buf[j + 3 * P / 4];
-      if (st > 0) {
-        const double2 w1 = tw[kk * (kFftPT / (4 * Ns))];
-        const double2 w2 = cmul(w1, w1), w3 = cmul(w2, w1);
-        v1 = cmul(v1, w1);
-        v2 = cmul(v2, w2);
-        v3 = cmul(v3, w3);
-      }
-      const double2 a0 = make_double2(v0.x + v2.x, v0.y + v2.y);
-      const double2 a1 = make_double2(v0.x - v2.x, v0.y - v2.y);
-      const double2 a2 = make_double2(v1.x + v3.x, v1.y + v3.y);
-      const double2 a3 = make_double2(v1.y - v3.y, v3.x - v1.x);  // (v1 − v3)·(−i)
-      y[m][0] = make_double2(a0.x + a2.x, a0.y + a2.y);
-      y[m][2] = make_double2(a0.x - a2.x, a0.y - a2.y);
-      y[m][1] = make_double2(a1.x + a3.x, a1.y + a3.y);
-      y[m][3] = make_double2(a1.x - a3.x, a1.y - a3.y);
-      base[m] = ((j - kk) << 2) + kk;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int m = 0; m < B4; ++m)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) buf[base[m] + r * Ns] = y[m][r];
-    __syncthreads();
+  for (int r = 0; r < 4; ++r) {
+    a[r] = make_double2(v[r].x + v[r + 4].x, v[r].y + v[r + 4].y);
+    c[r] = make_double2(v[r].x - v[r + 4].x, v[r].y - v[r + 4].y);
   }
-  if constexpr (LOGP & 1) {
-    // last stage, radix 2 (Ns = P/2): j < P/2, k = j
-    constexpr int B2 = E / 2;
-    double2 y0[B2], y1[B2];
+  // c1 ·= w8, c2 ·= −i, c3 ·= w8³
+  c[1] = make_double2((c[1].x + c[1].y) * h, (c[1].y - c[1].x) * h);
+  c[2] = make_double2(c[2].y, -c[2].x);
+  c[3] = make_double2((c[3].y - c[3].x) * h, -(c[3].x + c[3].y) * h);
+  // 4-point DFTs: evens from a, odds from c
+  auto dft4 = [](const double2 (&q)[4], double2& y0, double2& y1, double2& y2, double2& y3) {
+    const double2 t0 = make_double2(q[0].x + q[2].x, q[0].y + q[2].y);
+    const double2 t1 = make_double2(q[0].x - q[2].x, q[0].y - q[2].y);
+    const double2 t2 = make_double2(q[1].x + q[3].x, q[1].y + q[3].y);
+    const double2 t3 = make_double2(q[1].y - q[3].y, q[3].x - q[1].x);  // (q1 − q3)·(−i)
+    y0 = make_double2(t0.x + t2.x, t0.y + t2.y);
+    y2 = make_double2(t0.x - t2.x, t0.y - t2.y);
+    y1 = make_double2(t1.x + t3.x, t1.y + t3.y);
+    y3 = make_double2(t1.x - t3.x, t1.y - t3.y);
+  };
+  dft4(a, v[0], v[2], v[4], v[6]);
+  dft4(c, v[1], v[3], v[5], v[7]);
+}
+
+// In-place-in-registers Stockham FFT of P = 2^p points (forward), radix 8 (+ one radix-2 or
+// radix-4 stage when p mod 3 ≠ 0), by the first NF = P/8 threads of the workgroup: thread t
+// holds points t + NF·u (u = 0..7) on entry and the transform's points t + NF·u on exit, so
+// the first stage reads and the last stage writes registers; between stages the points pass
+// through LDS (buf, P complex).  Every thread of the workgroup must call it (barriers).
+template <int P>
+__device__ __forceinline__ void fft8(double2 (&v)[8], double2* buf,
+                                     const double2* __restrict__ tw, int tid) {
+  constexpr int NF = P / 8;
+  constexpr int LOGP = __builtin_ctz(P);
+  constexpr int A8 = LOGP / 3;  // radix-8 stages
+  constexpr int RL = LOGP % 3;  // last stage radix 2^RL (0: none)
+  constexpr int R = 1 << RL;
+  const bool act = tid < NF;
 #pragma unroll
-    for (int m = 0; m < B2; ++m) {
-      const int j = tid + NT * m;
-      const double2 v0 = buf[j];
-      const double2 v1 = cmul(buf[j + P / 2], tw[j * (kFftPT / P)]);
-      y0[m] = make_double2(v0.x + v1.x, v0.y + v1.y);
-      y1[m] = make_double2(v0.x - v1.x, v0.y - v1.y);
+  for (int st = 0; st < A8; ++st) {
+    const int Ns = 1 << (3 * st);
+    const int k = tid & (Ns - 1);
+    if (act) {
+      if (st > 0) {
+        const double2 w1 = tw[k * (kFftPT / (8 * Ns))];
+        const double2 w2 = cmul(w1, w1), w3 = cmul(w2, w1), w4 = cmul(w2, w2);
+        v[1] = cmul(v[1], w1);
+        v[2] = cmul(v[2], w2);
+        v[3] = cmul(v[3], w3);
+        v[4] = cmul(v[4], w4);
+        v[5] = cmul(v[5], cmul(w4, w1));
+        v[6] = cmul(v[6], cmul(w4, w2));
+        v[7] = cmul(v[7], cmul(w4, w3));
+      }
+      dft8(v);
     }
-    __syncthreads();
+    const bool last = (st == A8 - 1) && RL == 0;
+    if (!last) {
+      if (act) {
+        const int base = ((tid - k) << 3) + k;
 #pragma unroll
-    for (int m = 0; m < B2; ++m) {
-      const int j = tid + NT * m;
-      buf[j] = y0[m];
-      buf[j + P / 2] = y1[m];
+        for (int r = 0; r < 8; ++r) buf[base + r * Ns] = v[r];
+      }
+      __syncthreads();
+      if (act) {
+        if (st + 1 < A8) {
+#pragma unroll
+          for (int r = 0; r < 8; ++r) v[r] = buf[tid + r * NF];
+        } else {
+          // the radix-R stage: butterflies j = tid + NF·m (m < 8/R), inputs j + r·P/R
+#pragma unroll
+          for (int m = 0; m < 8 / R; ++m)
+#pragma unroll
+            for (int r = 0; r < R; ++r) v[m * R + r] = buf[tid + NF * m + r * (P / R)];
+        }
+      }
+      __syncthreads();
     }
-    __syncthreads();
+  }
+  if constexpr (RL > 0) {
+    // last stage (Ns = P/R, k = j): twiddles w^{r j}, w = e^{−2πi/P}; outputs j + r·P/R =
+    // tid + NF·(m + r·8/R)
+    double2 y[8];
+    if (act) {
+#pragma unroll
+      for (int m = 0; m < 8 / R; ++m) {
+        const int j = tid + NF * m;
+        const double2 w1 = tw[j * (kFftPT / P)];
+        double2 q[4];
+#pragma unroll
+        for (int r = 0; r < R; ++r) q[r] = v[m * R + r];
+        if constexpr (R == 2) {
+          q[1] = cmul(q[1], w1);
+          y[m] = make_double2(q[0].x + q[1].x, q[0].y + q[1].y);
+          y[m + 4] = make_double2(q[0].x - q[1].x, q[0].y - q[1].y);
+        } else {
+          const double2 w2 = cmul(w1, w1), w3 = cmul(w2, w1);
+          q[1] = cmul(q[1], w1);
+          q[2] = cmul(q[2], w2);
+          q[3] = cmul(q[3], w3);
+          const double2 t0 = make_double2(q[0].x + q[2].x, q[0].y + q[2].y);
+          const double2 t1 = make_double2(q[0].x - q[2].x, q[0].y - q[2].y);
+          const double2 t2 = make_double2(q[1].x + q[3].x, q[1].y + q[3].y);
+          const double2 t3 = make_double2(q[1].y - q[3].y, q[3].x - q[1].x);
+          y[m] = make_double2(t0.x + t2.x, t0.y + t2.y);
+          y[m + 2] = make_double2(t1.x + t3.x, t1.y + t3.y);
+          y[m + 4] = make_double2(t0.x - t2.x, t0.y - t2.y);
+          y[m + 6] = make_double2(t1.x - t3.x, t1.y - t3.y);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = y[u];
+    }
   }
 }
 
-// buf holds s (P complex) → f = conj(DFT(conj(DFT s)·G)) in place (G = the plan's DFT(g)/P).
-template <int NT, int E>
-__device__ __forceinline__ void fft_correlate(double2* buf, const double2* __restrict__ tw,
-                                              const double2* __restrict__ G, int tid) {
-  fft_forward<NT, E>(buf, tw, tid);
+// s (points t + NF·u in v, NF = P/8 threads) → f = conj(DFT(conj(DFT s)·G)) into buf (P complex,
+// natural order), G = the plan's DFT(g)/P.  Every thread of the workgroup must call it.
+template <int P>
+__device__ __forceinline__ void fft_correlate8(double2 (&v)[8], double2* buf,
+                                               const double2* __restrict__ tw,
+                                               const double2* __restrict__ G, int tid) {
+  constexpr int NF = P / 8;
+  fft8<P>(v, buf, tw, tid);
+  if (tid < NF) {
 #pragma unroll
-  for (int m = 0; m < E; ++m) {
-    const int q = tid + NT * m;
-    const double2 S = buf[q], g = G[q];
-    buf[q] = make_double2(fma(S.x, g.x, S.y * g.y), fma(S.x, g.y, -S.y * g.x));  // conj(S)·g
+    for (int u = 0; u < 8; ++u) {
+      const double2 S = v[u], g = G[tid + NF * u];
+      v[u] = make_double2(fma(S.x, g.x, S.y * g.y), fma(S.x, g.y, -S.y * g.x));  // conj(S)·g
+    }
+  }
+  __syncthreads();  // the last exchange's reads are done before buf is rewritten
+  fft8<P>(v, buf, tw, tid);
+  if (tid < NF) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) buf[tid + NF * u] = v[u];
   }
   __syncthreads();
-  fft_forward<NT, E>(buf, tw, tid);
 }
 
 // Long walks (64·8+1 < n ≤ 64·8·8+1): the split-axis structure widened to W waves per axis
@@ -970,18 +1035,21 @@ __global__ void __launch_bounds__(128 * W, 4) zmpc_rollout_unc_wide_kernel(Rollo
     double2* buf = reinterpret_cast<double2*>(smem);
     const double2* zmx = reinterpret_cast<const double2*>(a.zmax + b * a.bstride);
     const double2* zmn = reinterpret_cast<const double2*>(a.zmin + b * a.bstride);
-    double2 hi[E], lo[E];
+    constexpr int P = NT * E, NF = P / 8;  // the first NF threads run the transform
+    double2 v[8];
+    if (tid < NF) {
+      double2 hi[8], lo[8];
 #pragma unroll
-    for (int u = 0; u < E; ++u) {
-      const int tc = min(u * NT + tid, n - 1);
-      hi[u] = zmx[tc];
-      lo[u] = zmn[tc];
+      for (int u = 0; u < 8; ++u) {
+        const int tc = min(tid + NF * u, n - 1);
+        hi[u] = zmx[tc];
+        lo[u] = zmn[tc];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        v[u] = make_double2((hi[u].x + lo[u].x) / 2, (hi[u].y + lo[u].y) / 2);
     }
-#pragma unroll
-    for (int u = 0; u < E; ++u)
-      buf[u * NT + tid] = make_double2((hi[u].x + lo[u].x) / 2, (hi[u].y + lo[u].y) / 2);
-    __syncthreads();
-    fft_correlate<NT, E>(buf, a.fft_tw, a.fft_g, tid);
+    fft_correlate8<P>(v, buf, a.fft_tw, a.fft_g, tid);
 #pragma unroll
     for (int q = 0; q < CW; ++q) {
       const double2 c = buf[min(mbeg + q, NT * E - 1)];
