@@ -104,3 +104,20 @@ def test_herdt_find_nb_steps_drop_in():
     assert np.array_equal(np.array(c.find_nb_steps(pad)), d["nb_steps"])
     A, b = c._polytope_halfspace(np.array(MPCConfig().left_foot_polytope))
     assert np.array_equal(A, d["poly_left_A"])
+
+
+def test_herdt_work_counters():
+    """zmpc_plan_counters [4..7]: every solve of both axes takes at least one active-set pass,
+    and the footstep sums match the windows' counts of the default walk."""
+    d = golden("herdt_default.npz")
+    c = ZMPController(MPCConfig(method="herdt", add_force=True))
+    plan = c._plan()
+    plan.counters(reset=True)
+    B = 32
+    F = np.linspace(0.0, 800.0, B)
+    c.generate_com_trajectory_herdt_batch(None, d["v_ref"], d["states"], F_ext=F)
+    k = plan.counters(reset=True)
+    n = len(d["states"])
+    assert k["herdt_instance_passes"] >= 2 * B * (n - 1)
+    assert k["herdt_wave_passes"] * 64 >= k["herdt_instance_passes"]
+    assert k["herdt_footsteps_sq"] >= k["herdt_footsteps"] >= 0

@@ -642,3 +642,45 @@ def test_strict_cholesky_variant_vs_oracle():
                                      "strict_long_oracle.npz")],
                        env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0 and "CHOL_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+
+
+_DIRECT_CHILD = r"""
+import sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+import torch
+from mpc_bipedal.solver import Plan
+d = np.load(sys.argv[2])
+p = Plan(0, int(d["N"]), float(d["dt"]), 0.75, 9.81, 1.0, 1e-6, False)
+h, _ = p.rollout(d["zmax"], d["zmin"], d["x0"], kick=d["kick"], kick_step=int(d["ks"]))
+np.save(sys.argv[3], h.cpu().numpy())
+print("DIRECT_OK")
+"""
+
+
+@pytest.mark.parametrize("N,n", ((512, 1431), (150, 1100), (150, 2500)))
+def test_fft_correlation_equals_direct(N, n, tmp_path):
+    """Long walks take the FFT correlation (rollout.hip, wide kernel); the direct form
+    (ZMPC_NO_FFT=1, in a subprocess) on the same batch agrees to rounding: max |Δ| ≤ 1e-11
+    on O(1) states (measured ≈1e-14)."""
+    import subprocess
+    import sys
+    rng = np.random.default_rng(n)
+    dt = 1.5 / N if N == 512 else 0.01
+    B = 8
+    zc = np.cumsum(rng.uniform(-0.01, 0.01, (B, n, 2)), axis=1)
+    zmax, zmin = zc + 0.05, zc - 0.05
+    x0 = np.zeros((B, 2, 3))
+    x0[:, :, 0] = rng.uniform(-0.01, 0.01, (B, 2))
+    kick = dt * rng.uniform(0, 800, B) / M
+    f = tmp_path / "in.npz"
+    np.savez(f, zmax=zmax, zmin=zmin, x0=x0, kick=kick, N=N, dt=dt, ks=n // 2)
+    p = plan(N, dt=dt)
+    h_fft, _ = p.rollout(zmax, zmin, x0, kick=kick, kick_step=n // 2)
+    out = tmp_path / "direct.npy"
+    env = dict(os.environ, ZMPC_NO_FFT="1")
+    r = subprocess.run([sys.executable, "-c", _DIRECT_CHILD, PKG, str(f), str(out)], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "DIRECT_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+    h_dir = np.load(out)
+    assert np.abs(h_fft.cpu().numpy() - h_dir).max() <= 1e-11
