@@ -411,51 +411,79 @@ __device__ __forceinline__ void seg_sweep_b(const LqArgs& a, int j, Ric& v, cons
   seg_costate<S, FULL>(a, j, in, g, lam, changed, kl, fl, lane);
 }
 
-__device__ __forceinline__ void ck_store(double* ck, int j, const Ric& v, int lane) {
+// Checkpoints are written once and read once per pass.  With per-walk bounds (whose rows are
+// re-read every timestep and do not fit the caches) they go non-temporal (NT), so they do not
+// push those rows out; with a shared CoP the bounds are cache-resident anyway and the
+// checkpoints are better off cached (config 3: 98.8 → 92.2 ms NT; config 4: 142 → 158 ms NT).
+template <bool NT>
+struct CkIO {
+  __device__ __forceinline__ void st(double* p, double v) const {
+    if constexpr (NT)
+      __builtin_nontemporal_store(v, p);
+    else
+      *p = v;
+  }
+  __device__ __forceinline__ double ld(const double* p) const {
+    if constexpr (NT)
+      return __builtin_nontemporal_load(p);
+    else
+      return *p;
+  }
+};
+
+template <bool NT>
+__device__ __forceinline__ void ck_store(const CkIO<NT>& io, double* ck, int j, const Ric& v,
+                                         int lane) {
   double* p = ck + (size_t)j * 9 * 64 + lane;
-  p[0] = v.p00;
-  p[64] = v.p01;
-  p[128] = v.p02;
-  p[192] = v.p11;
-  p[256] = v.p12;
-  p[320] = v.p22;
-  p[384] = v.s0;
-  p[448] = v.s1;
-  p[512] = v.s2;
+  io.st(p + 0, v.p00);
+  io.st(p + 64, v.p01);
+  io.st(p + 128, v.p02);
+  io.st(p + 192, v.p11);
+  io.st(p + 256, v.p12);
+  io.st(p + 320, v.p22);
+  io.st(p + 384, v.s0);
+  io.st(p + 448, v.s1);
+  io.st(p + 512, v.s2);
 }
 
-__device__ __forceinline__ void ck_store_s(double* ck, int j, const Ric& v, int lane) {
+template <bool NT>
+__device__ __forceinline__ void ck_store_s(const CkIO<NT>& io, double* ck, int j, const Ric& v,
+                                           int lane) {
   double* p = ck + (size_t)j * 9 * 64 + lane;
-  p[384] = v.s0;
-  p[448] = v.s1;
-  p[512] = v.s2;
+  io.st(p + 384, v.s0);
+  io.st(p + 448, v.s1);
+  io.st(p + 512, v.s2);
 }
 
-__device__ __forceinline__ void ck_load(const double* ck, int j, Ric& v, int lane) {
+template <bool NT>
+__device__ __forceinline__ void ck_load(const CkIO<NT>& io, const double* ck, int j, Ric& v,
+                                        int lane) {
   const double* p = ck + (size_t)j * 9 * 64 + lane;
-  v.p00 = p[0];
-  v.p01 = p[64];
-  v.p02 = p[128];
-  v.p11 = p[192];
-  v.p12 = p[256];
-  v.p22 = p[320];
-  v.s0 = p[384];
-  v.s1 = p[448];
-  v.s2 = p[512];
+  v.p00 = io.ld(p + 0);
+  v.p01 = io.ld(p + 64);
+  v.p02 = io.ld(p + 128);
+  v.p11 = io.ld(p + 192);
+  v.p12 = io.ld(p + 256);
+  v.p22 = io.ld(p + 320);
+  v.s0 = io.ld(p + 384);
+  v.s1 = io.ld(p + 448);
+  v.s2 = io.ld(p + 512);
 }
 
-__device__ __forceinline__ void ck_load_s(const double* ck, int j, Ric& v, int lane) {
+template <bool NT>
+__device__ __forceinline__ void ck_load_s(const CkIO<NT>& io, const double* ck, int j, Ric& v,
+                                          int lane) {
   const double* p = ck + (size_t)j * 9 * 64 + lane;
-  v.s0 = p[384];
-  v.s1 = p[448];
-  v.s2 = p[512];
+  v.s0 = io.ld(p + 384);
+  v.s1 = io.ld(p + 448);
+  v.s2 = io.ld(p + 512);
 }
 
 // G waves per workgroup.  G = 8: waves 0..3 take the x axis and 4..7 the y axis of the same
 // four 64-walk groups, so each SIMD (waves w and w + 4 under the round-robin placement) holds
 // one wave of each axis — the y axis carries nearly all of the active-set work, and an
 // axis-pure SIMD would idle once its x waves are done.  G = 4 (A/B): axis = wave parity.
-template <int S, int W, int G>
+template <int S, int W, int G, bool NT = false>
 __global__ void __launch_bounds__(64 * G, W)
     zmpc_strict_lq_kernel(LqArgs a, const double* __restrict__ tab) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lq_smem[];
@@ -465,6 +493,7 @@ __global__ void __launch_bounds__(64 * G, W)
   // slot flags [NS·S][64] (rows past N stay 0: the last segment's loads are unguarded)
   unsigned char* fl = lq_smem + (size_t)wave * a.NS * S * 64;
   double* ck = a.ck + (size_t)gw * a.NS * 9 * 64;
+  const CkIO<NT> io{};
   int axis;
   int64_t b0;
   if (a.window_mode) {
@@ -541,7 +570,7 @@ __global__ void __launch_bounds__(64 * G, W)
 #pragma unroll 1
         for (int j = a.NS - 1; j >= jt; --j) {
           seg_load<S, false>(a, j, L, i, fl, cur);
-          ck_store_s(ck, j, v, lane);
+          ck_store_s(io, ck, j, v, lane);
           if (j < jfull)
             seg_tail<S, true, false>(a, tab, j, v, cur, g);
           else
@@ -560,7 +589,7 @@ __global__ void __launch_bounds__(64 * G, W)
 #pragma unroll 1
         for (int j = jt - 1; j >= 0; --j) {
           seg_load<S, true>(a, j, L, i, fl, cur);
-          ck_store(ck, j, v, lane);
+          ck_store(io, ck, j, v, lane);
           const bool fr = seg_free(cur);
           if (j < jfull) {
             if (fr)
@@ -580,7 +609,7 @@ __global__ void __launch_bounds__(64 * G, W)
 #pragma unroll 1
         for (int j = 0; j < jt; ++j) {
           seg_load<S, true>(a, j, L, i, fl, cur);
-          ck_load(ck, j, v, lane);
+          ck_load(io, ck, j, v, lane);
           // (a free form here, as in sweep A, costs more registers than it saves)
           if (j < jfull)
             seg_sweep_b<S, true>(a, j, v, cur, g, xs, u0, changed, kl, fl, lane);
@@ -590,7 +619,7 @@ __global__ void __launch_bounds__(64 * G, W)
 #pragma unroll 1
         for (int j = jt; j < a.NS; ++j) {
           seg_load<S, false>(a, j, L, i, fl, cur);
-          ck_load_s(ck, j, v, lane);
+          ck_load_s(io, ck, j, v, lane);
           if (j < jfull) {
             seg_tail<S, true, true>(a, tab, j, v, cur, g);
             seg_forward_tail<S, true>(a, tab, j, cur, g, xs, u0, changed, kl, fl, lane);
@@ -734,17 +763,21 @@ hipError_t stage(const double* hi, const double* lo, int64_t sb, int64_t st, int
 // A/B only; default below).
 struct LqVariant {
   int S, W, G;
-  void (*kernel)(LqArgs, const double*);
+  void (*kernel)(LqArgs, const double*);     // checkpoints cached (shared CoP, window mode)
+  void (*kernel_nt)(LqArgs, const double*);  // checkpoints non-temporal (per-walk bounds)
 };
 
+#define ZMPC_LQV(S, W, G) \
+  {S, W, G, zmpc_strict_lq_kernel<S, W, G, false>, zmpc_strict_lq_kernel<S, W, G, true>}
 const LqVariant kLqVariants[] = {
-    {8, 2, 8, zmpc_strict_lq_kernel<8, 2, 8>},  // default
-    {8, 2, 4, zmpc_strict_lq_kernel<8, 2, 4>},  // N up to 640 (slot flags of 4 waves in LDS)
-    {8, 2, 2, zmpc_strict_lq_kernel<8, 2, 2>},  // N up to 1280
-    {8, 2, 1, zmpc_strict_lq_kernel<8, 2, 1>},  // N up to 2560
-    {6, 2, 8, zmpc_strict_lq_kernel<6, 2, 8>},
-    {8, 1, 8, zmpc_strict_lq_kernel<8, 1, 8>},
+    ZMPC_LQV(8, 2, 8),  // default
+    ZMPC_LQV(8, 2, 4),  // N up to 640 (slot flags of 4 waves in LDS)
+    ZMPC_LQV(8, 2, 2),  // N up to 1280
+    ZMPC_LQV(8, 2, 1),  // N up to 2560
+    ZMPC_LQV(6, 2, 8),
+    ZMPC_LQV(8, 1, 8),
 };
+#undef ZMPC_LQV
 constexpr size_t kLdsCap = 160 * 1024;
 
 LqVariant lq_variant() {
@@ -771,7 +804,7 @@ LqVariant lq_variant_for(int N) {
   for (int g = v.G / 2; g >= 1; g /= 2)
     for (const LqVariant& c : kLqVariants)
       if (c.S == v.S && c.W == v.W && c.G == g && (size_t)g * rows * 64 <= kLdsCap) return c;
-  return LqVariant{v.S, v.W, 0, nullptr};
+  return LqVariant{v.S, v.W, 0, nullptr, nullptr};
 }
 
 void fill_consts(const zmpc_plan* p, LqArgs& a) {
@@ -806,8 +839,10 @@ hipError_t launch_lq(const zmpc_plan* p, LqArgs& a, int64_t waves, hipStream_t s
   const LqVariant var = lq_variant_for(p->N);
   const int64_t blocks = (waves + var.G - 1) / var.G;
   const size_t lds = (size_t)var.G * a.NS * var.S * 64;
-  hipLaunchKernelGGL(var.kernel, dim3((unsigned)blocks), dim3(64 * var.G), lds, s, a,
-                     (const double*)p->lqtab);
+  // rollouts over per-walk bounds: non-temporal checkpoints (see CkIO)
+  const bool nt = !a.window_mode && !a.shared;
+  hipLaunchKernelGGL(nt ? var.kernel_nt : var.kernel, dim3((unsigned)blocks), dim3(64 * var.G),
+                     lds, s, a, (const double*)p->lqtab);
   hipError_t e = hipGetLastError();
   if (dbg_on && a.cnt && e == hipSuccess) {
     unsigned long long h[4];
@@ -826,9 +861,10 @@ hipError_t launch_lq(const zmpc_plan* p, LqArgs& a, int64_t waves, hipStream_t s
 hipError_t zmpc_strict_lq_set_attrs() {
   hipError_t e = hipSuccess;
   for (const LqVariant& c : kLqVariants)
-    if (e == hipSuccess)
-      e = hipFuncSetAttribute((const void*)c.kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              160 * 1024);
+    for (auto k : {c.kernel, c.kernel_nt})
+      if (e == hipSuccess)
+        e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                160 * 1024);
   return e;
 }
 
