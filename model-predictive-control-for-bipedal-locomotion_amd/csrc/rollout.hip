@@ -22,7 +22,6 @@
 //   4. each lane replays its chunk in the reference form x⁺ = A x + B u with the F_ext kick
 //      (:105-106); history rows are staged in LDS and leave as contiguous 1-KiB wave stores.
 // Walks longer than 64·8+1 samples take several correlation passes with f kept in LDS.
-#include <vector>
 #include <algorithm>
 #include <climits>
 #include <cstdint>
@@ -845,68 +844,12 @@ template <int CW, bool SHF = false>
 __global__ void __launch_bounds__(128, 4)
     zmpc_rollout_unc_pers_kernel(RolloutArgs a, const double* __restrict__ kg,
                                  const double* __restrict__ scanP,
-                                 const double* __restrict__ kxp, double* __restrict__ hist,
-                                 int stag, int stag_mode, unsigned* ctr,
-                                 unsigned long long* trace) {
+                                 const double* __restrict__ kxp, double* __restrict__ hist) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   __shared__ int flag[2];
-  __shared__ int64_t next_b;
-  // diagnostic (ZMPC_PERS_TRACE): per workgroup HW_ID, XCC_ID, and the clock at start and
-  // after each walk (s_memtime, core clock; s_memrealtime, 100 MHz)
-  unsigned long long* tr = trace ? trace + (size_t)blockIdx.x * 8 : nullptr;
-  if (tr && threadIdx.x == 0) {
-    tr[0] = __builtin_amdgcn_s_getreg(0xF804);
-    tr[1] = __builtin_amdgcn_s_getreg(0xF814);
-    tr[2] = __builtin_amdgcn_s_memrealtime();
-    tr[3] = __builtin_amdgcn_s_memtime();
-  }
-  int wi = 0;
-  // A/B (ZMPC_PERS_STAGGER): delay one group of workgroups so that its loads overlap the other
-  // group's correlation instead of every CU running load / compute / store in lockstep
-  if (stag > 0) {
-    const unsigned g = stag_mode == 0 ? (blockIdx.x >= gridDim.x / 2)
-                                      : ((blockIdx.x / stag_mode) & 1u);
-    if (g)
-      for (int i = 0; i < stag; ++i) __builtin_amdgcn_s_sleep(16);
-  }
-  const int prio = stag_mode >> 16;
-  if (prio) __builtin_amdgcn_s_setprio(2);
-  if (ctr == nullptr) {
-    for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x) {
-      split_walk<CW, SHF>(a, b, smem, flag, kg, scanP, kxp, hist);
-      __syncthreads();  // staging read out before the next walk's z_ref overwrites it
-      if (tr && threadIdx.x == 0 && wi < 4) tr[4 + wi] = __builtin_amdgcn_s_memtime();
-      ++wi;
-      // A/B: a wave that has finished more walks yields the SIMD to the ones behind it
-      if (prio) {
-        if (wi == 1) __builtin_amdgcn_s_setprio(1);
-        else __builtin_amdgcn_s_setprio(0);
-      }
-    }
-  } else if (stag_mode & 0x8000) {
-    // dynamic queue per XCD (workgroups go round-robin over the 8 XCDs): walks b ≡ x mod 8
-    const int x = blockIdx.x & 7;
-    const int64_t nx = (a.B - x + 7) / 8;
-    int64_t j = blockIdx.x >> 3;
-    while (j < nx) {
-      split_walk<CW, SHF>(a, x + 8 * j, smem, flag, kg, scanP, kxp, hist);
-      if (threadIdx.x == 0) next_b = (int64_t)(gridDim.x >> 3) + atomicAdd(ctr + 64 * x, 1u);
-      __syncthreads();
-      j = next_b;
-      if (tr && threadIdx.x == 0 && wi < 4) tr[4 + wi] = __builtin_amdgcn_s_memtime();
-      ++wi;
-      __syncthreads();
-    }
-  } else {
-    // dynamic walk queue: the first walk is blockIdx, later ones from the launch counter
-    int64_t b = blockIdx.x;
-    while (b < a.B) {
-      split_walk<CW, SHF>(a, b, smem, flag, kg, scanP, kxp, hist);
-      if (threadIdx.x == 0) next_b = (int64_t)gridDim.x + atomicAdd(ctr, 1u);
-      __syncthreads();
-      b = next_b;
-      __syncthreads();
-    }
+  for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x) {
+    split_walk<CW, SHF>(a, b, smem, flag, kg, scanP, kxp, hist);
+    __syncthreads();  // staging read out before the next walk's z_ref overwrites it
   }
 }
 
@@ -1573,40 +1516,8 @@ void launch_unc(const RolloutGeom& g, size_t lds, hipStream_t s, const RolloutAr
     // persistent only for a few walks per workgroup: config 2 (2 per workgroup) 45 µs vs
     // 49 µs; at 8 per workgroup (B = 16384) the one-walk grid is faster (156 vs 177 µs)
     if (per_cu > 0 && grid < a.B && a.B <= 3 * grid) {
-      static const char* trace_path = getenv("ZMPC_PERS_TRACE");  // diagnostic only
-      unsigned long long* trace = nullptr;
-      if (trace_path) {
-        (void)hipMalloc(&trace, (size_t)grid * 8 * sizeof(unsigned long long));
-        (void)hipMemsetAsync(trace, 0, (size_t)grid * 8 * sizeof(unsigned long long), s);
-      }
-      static int stag = 0, stag_mode = 0, dyn = 0;
-      static const bool stag_init = [] {
-        const char* e = getenv("ZMPC_PERS_STAGGER");  // A/B only: "units,mode,dyn"
-        if (e) sscanf(e, "%d,%d,%d", &stag, &stag_mode, &dyn);
-        return true;
-      }();
-      (void)stag_init;
-      unsigned* ctr = nullptr;
-      if (dyn) {
-        static unsigned* c = nullptr;
-        if (c == nullptr) (void)hipMalloc(&c, 512 * sizeof(unsigned));
-        (void)hipMemsetAsync(c, 0, 512 * sizeof(unsigned), s);
-        ctr = c;
-      }
       hipLaunchKernelGGL(zmpc_rollout_unc_pers_kernel<CW>, dim3((unsigned)grid), dim3(128),
-                         lds_split, s, a, a.k, a.scanP, a.kx, a.hist, stag, stag_mode, ctr,
-                         trace);
-      if (trace) {
-        std::vector<unsigned long long> h((size_t)grid * 8);
-        (void)hipStreamSynchronize(s);
-        (void)hipMemcpy(h.data(), trace, h.size() * sizeof(unsigned long long),
-                        hipMemcpyDeviceToHost);
-        (void)hipFree(trace);
-        if (FILE* fp = fopen(trace_path, "wb")) {
-          fwrite(h.data(), sizeof(unsigned long long), h.size(), fp);
-          fclose(fp);
-        }
-      }
+                         lds_split, s, a, a.k, a.scanP, a.kx, a.hist);
     } else {
       hipLaunchKernelGGL(zmpc_rollout_unc_split_kernel<CW>, dim3((unsigned)a.B), dim3(128),
                          lds_split, s, a);
