@@ -89,6 +89,8 @@ def fft_transform(n, N):
     E = P // (128 * W) if P % (128 * W) == 0 else 0
     if E not in (4, 8) or P > 8192 or P * 16 > 64 * 1024:
         return None
+    if ns * N < 9 * P * int(np.log2(P)):  # measured crossover: the direct form is faster
+        return None
     return P
 
 

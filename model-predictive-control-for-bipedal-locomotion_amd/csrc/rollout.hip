@@ -1015,7 +1015,7 @@ __device__ __forceinline__ void fft_correlate8(double2 (&v)[8], double2* buf,
 // waves' end states with M = (Ā^CW)^64 (plan level 6), and lane l adds (Ā^CW)^(l+1)·x_start by
 // binary powering.  History staged through the z_ref area in rounds (replay per round).
 template <int CW, int W, int E = 0>
-__global__ void __launch_bounds__(128 * W, 4) zmpc_rollout_unc_wide_kernel(RolloutArgs a) {
+__global__ void __launch_bounds__(128 * W, E == 4 ? 6 : 4) zmpc_rollout_unc_wide_kernel(RolloutArgs a) {
   using ZL = ZrLayout<CW>;
   constexpr int NT = 128 * W;
   extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -1575,13 +1575,21 @@ hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, con
     q.lzp = wg.lzp;
     size_t lds_w = 2 * (size_t)wg.lzp * sizeof(double);
     // FFT correlation when the transform maps onto the workgroup (E = P/NT points per thread,
-    // 4 or 8) and fits the default LDS ceiling; ZMPC_NO_FFT keeps the direct form (A/B)
-    static const bool no_fft = getenv("ZMPC_NO_FFT") != nullptr;
+    // 4 or 8), fits the default LDS ceiling and costs less than the direct form: measured
+    // crossover (n − 1)·N ≥ 9·P·log2 P — N = 150 walks of 1000/2000 samples
+    // are faster direct, N ≥ 200 faster by FFT.  ZMPC_FFT=0/1 forces the direct form / the FFT
+    // wherever it fits (A/B and tests; ZMPC_NO_FFT = ZMPC_FFT=0).
+    static const int fft_mode = [] {
+      if (getenv("ZMPC_NO_FFT") != nullptr) return 0;
+      const char* e = getenv("ZMPC_FFT");
+      return e ? atoi(e) : -1;
+    }();
     int P = kFftPmin;
     while (P < n - 1 + p->N) P *= 2;
     const int NT = 128 * wg.w;
     int E = (P % NT == 0) ? P / NT : 0;
-    if (no_fft || (E != 4 && E != 8) || P > kFftPT || (size_t)P * 16 > 64 * 1024) E = 0;
+    if (fft_mode == 0 || (E != 4 && E != 8) || P > kFftPT || (size_t)P * 16 > 64 * 1024) E = 0;
+    if (fft_mode < 0 && (double)(n - 1) * p->N < 9.0 * P * __builtin_ctz((unsigned)P)) E = 0;
     if (E) {
       q.fft_tw = reinterpret_cast<const double2*>(p->fft_tw);
       q.fft_g = reinterpret_cast<const double2*>(p->fft_g) + (P - kFftPmin);

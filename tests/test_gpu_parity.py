@@ -658,11 +658,13 @@ print("DIRECT_OK")
 """
 
 
-@pytest.mark.parametrize("N,n", ((512, 1431), (150, 1100), (150, 2500)))
+@pytest.mark.parametrize("N,n", ((512, 1431), (150, 1100), (150, 2500), (256, 1000),
+                                 (200, 3000)))
 def test_fft_correlation_equals_direct(N, n, tmp_path):
-    """Long walks take the FFT correlation (rollout.hip, wide kernel); the direct form
-    (ZMPC_NO_FFT=1, in a subprocess) on the same batch agrees to rounding: max |Δ| ≤ 1e-11
-    on O(1) states (measured ≈1e-14)."""
+    """Long walks: the FFT correlation (rollout.hip, wide kernel; forced with ZMPC_FFT=1 in a
+    subprocess) and the direct form (ZMPC_FFT=0, in a subprocess) on the same batch agree to
+    rounding: max |Δ| ≤ 1e-11 on O(1) states (measured ≈1e-14); the automatic choice (this
+    process: FFT where (n − 1)·N ≥ 9·P·log2 P, e.g. N ≥ 200 here) equals one of them exactly."""
     import subprocess
     import sys
     rng = np.random.default_rng(n)
@@ -676,11 +678,16 @@ def test_fft_correlation_equals_direct(N, n, tmp_path):
     f = tmp_path / "in.npz"
     np.savez(f, zmax=zmax, zmin=zmin, x0=x0, kick=kick, N=N, dt=dt, ks=n // 2)
     p = plan(N, dt=dt)
-    h_fft, _ = p.rollout(zmax, zmin, x0, kick=kick, kick_step=n // 2)
-    out = tmp_path / "direct.npy"
-    env = dict(os.environ, ZMPC_NO_FFT="1")
-    r = subprocess.run([sys.executable, "-c", _DIRECT_CHILD, PKG, str(f), str(out)], env=env,
-                       capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0 and "DIRECT_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
-    h_dir = np.load(out)
-    assert np.abs(h_fft.cpu().numpy() - h_dir).max() <= 1e-11
+    h_auto, _ = p.rollout(zmax, zmin, x0, kick=kick, kick_step=n // 2)
+    h = {}
+    for mode in ("1", "0"):
+        out = tmp_path / f"fft{mode}.npy"
+        env = dict(os.environ, ZMPC_FFT=mode)
+        env.pop("ZMPC_NO_FFT", None)
+        r = subprocess.run([sys.executable, "-c", _DIRECT_CHILD, PKG, str(f), str(out)],
+                           env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0 and "DIRECT_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
+        h[mode] = np.load(out)
+    assert np.abs(h["1"] - h["0"]).max() <= 1e-11
+    h_auto = h_auto.cpu().numpy()
+    assert np.array_equal(h_auto, h["1"]) or np.array_equal(h_auto, h["0"])
