@@ -665,7 +665,10 @@ __global__ void __launch_bounds__(128, 8) zmpc_rollout_unc_axis_kernel(RolloutAr
 // One walk of the split kernel (shared by the one-walk-per-workgroup and the persistent
 // launch).  The tables read on wave-uniform addresses come in as __restrict__ pointers so the
 // compiler keeps them on scalar loads even inside a loop that stores the history.
-template <int CW, bool SHF = false>
+// PM (the persistent kernel): the walk's global loads and its history copy-out are issued at
+// raised wave priority, so a CU's co-resident walks get their memory traffic out ahead of the
+// others' correlation (config 2: 45.3 → 43.8 µs; the one-walk-per-workgroup grid is not helped).
+template <int CW, bool SHF = false, bool PM = false>
 __device__ __forceinline__ void split_walk(const RolloutArgs& a, int64_t b, double* smem,
                                            int* flag, const double* __restrict__ kg,
                                            const double* __restrict__ scanP,
@@ -687,10 +690,12 @@ __device__ __forceinline__ void split_walk(const RolloutArgs& a, int64_t b, doub
     double* zr0 = smem;
     double* zr1 = zr0 + a.lzp;
     // ---- 1. loads --------------------------------------------------------------------------
+    if constexpr (PM) __builtin_amdgcn_s_setprio(3);  // issue the walk's loads first
     AxisBounds<CW> r;
     axis_load<CW>(a, b, tid, r);
     const double2 hl = reinterpret_cast<const double2*>(a.zmax + b * a.bstride)[n - 1];
     const double2 ll = reinterpret_cast<const double2*>(a.zmin + b * a.bstride)[n - 1];
+    if constexpr (PM) __builtin_amdgcn_s_setprio(0);
     // ---- 2. z_ref rows + window padding (zmp_controller.py:81-88) --------------------------
 #pragma unroll
     for (int u = 0; u < AxisBounds<CW>::PF2; ++u) {
@@ -801,9 +806,20 @@ __device__ __forceinline__ void split_walk(const RolloutArgs& a, int64_t b, doub
   __syncthreads();
   // ---- 6. coalesced copy-out ---------------------------------------------------------------
   if (!(a.dbg & 4)) {
+    if constexpr (PM) __builtin_amdgcn_s_setprio(3);
     const double2* src = reinterpret_cast<const double2*>(stage);
     double2* dst = reinterpret_cast<double2*>(hist + b * (int64_t)n * 6);
-    for (int e = tid; e < n * 3; e += 128) dst[e] = src[e];
+    // four rows in flight per thread (LDS reads batched ahead of the stores)
+    int e = tid;
+    for (; e + 3 * 128 < n * 3; e += 4 * 128) {
+      const double2 v0 = src[e], v1 = src[e + 128], v2 = src[e + 256], v3 = src[e + 384];
+      dst[e] = v0;
+      dst[e + 128] = v1;
+      dst[e + 256] = v2;
+      dst[e + 384] = v3;
+    }
+    for (; e < n * 3; e += 128) dst[e] = src[e];
+    if constexpr (PM) __builtin_amdgcn_s_setprio(0);
   }
   if (a.status != nullptr && tid == 0) a.status[b] = flag[0] | flag[1];
 }
@@ -848,7 +864,7 @@ __global__ void __launch_bounds__(128, 4)
   extern __shared__ __attribute__((aligned(16))) double smem[];
   __shared__ int flag[2];
   for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x) {
-    split_walk<CW, SHF>(a, b, smem, flag, kg, scanP, kxp, hist);
+    split_walk<CW, SHF, true>(a, b, smem, flag, kg, scanP, kxp, hist);
     __syncthreads();  // staging read out before the next walk's z_ref overwrites it
   }
 }
