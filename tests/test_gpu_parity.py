@@ -458,8 +458,11 @@ def test_full_size_config2_properties():
 
 
 @pytest.mark.parametrize("N", (16, 64, 150))
-def test_strict_step_vs_oracle(N):
-    d = golden("strict_oracle.npz")
+def test_strict_step_vs_reference(N):
+    """Cold strict predict_wieber_axis calls with heavily active bounds vs the state the
+    reference's own strict branch returned (tests/golden/strict_ref.npz: the reference's QP,
+    captured by a recording cvxpy stand-in and answered exactly — make_strict_ref_golden.py)."""
+    d = golden("strict_ref.npz")
     p = plan(N, strict=True)
     out, st = p.step(d[f"step{N}_x"], d[f"step{N}_zmax"], d[f"step{N}_zmin"])
     ref = d[f"step{N}_out"]
@@ -469,32 +472,33 @@ def test_strict_step_vs_oracle(N):
 
 @pytest.mark.parametrize("N", (64, 150))
 @pytest.mark.parametrize("F", (0, 400, 800))
-def test_strict_rollout_vs_oracle(N, F):
-    d = golden("strict_oracle.npz")
+def test_strict_rollout_vs_reference(N, F):
+    """generate_com_trajectory(strict=True) on the default walk vs the reference-driven strict
+    rollout (strict_ref.npz): CoM and ZMP RMSE <= 1e-9 for every F_ext (north star: 1e-6)."""
+    d = golden("strict_ref.npz")
     zx, zn = d[f"n{N}_zmax"], d[f"n{N}_zmin"]
-    n = len(zx)
-    dt = 1.5 / N
     cfg = MPCConfig(horizon=N, strict=True, add_force=F > 0, F_ext=float(F))
     c = ZMPController(cfg)
     com, y_hist = c.generate_com_trajectory(np.zeros((3, 1)), np.zeros((3, 1)), zx, zn)
-    ref = d[f"n{N}_F{F}_hist"]
-    assert rmse(com, ref[:, :, 0]) <= 1e-6
-    assert rmse(com, ref[:, :, 0]) <= 1e-9 or F == 800
+    assert rmse(com, d[f"n{N}_F{F}_com"]) <= 1e-9
     zmp = y_hist[:, :, 0] @ c.C
-    assert rmse(zmp, ref[:, 1, :] @ c.C) <= 1e-6
+    assert rmse(zmp, d[f"n{N}_F{F}_yhist"] @ c.C) <= 1e-9
+    assert np.abs(y_hist[:, :, 0] - d[f"n{N}_F{F}_yhist"]).max() <= 1e-6
     # the planned ZMP respects the bounds (strict semantics)
     assert np.all(zmp[1:] <= zx[1:, 1] + 1e-9) and np.all(zmp[1:] >= zn[1:, 1] - 1e-9)
 
 
 @pytest.mark.parametrize("N", (64, 150))
-def test_strict_rollout_x0_vs_oracle(N):
-    d = golden("strict_oracle.npz")
+def test_strict_state_trajectory_x0_vs_reference(N):
+    d = golden("strict_ref.npz")
     c = ZMPController(MPCConfig(horizon=N, strict=True))
-    xs, ys = c.generate_state_trajectory_wieber(d[f"n{N}_x0"], d[f"n{N}_y0"], d[f"n{N}_zmax"],
+    xs, ys = c.generate_state_trajectory_wieber(d[f"n{N}_x0"].reshape(3, 1),
+                                                d[f"n{N}_y0"].reshape(3, 1), d[f"n{N}_zmax"],
                                                 d[f"n{N}_zmin"])
-    ref = d[f"n{N}_x0_hist"]
-    assert rmse(xs[:, 0, 0], ref[:, 0, 0]) <= 1e-9
-    assert rmse(ys[:, 0, 0], ref[:, 1, 0]) <= 1e-9
+    assert rmse(xs[:, 0, 0], d[f"n{N}_x0_xhist"][:, 0]) <= 1e-9
+    assert rmse(ys[:, 0, 0], d[f"n{N}_x0_yhist"][:, 0]) <= 1e-9
+    assert np.abs(xs[:, :, 0] - d[f"n{N}_x0_xhist"]).max() <= 1e-6
+    assert np.abs(ys[:, :, 0] - d[f"n{N}_x0_yhist"]).max() <= 1e-6
 
 
 def test_strict_equals_unconstrained_when_inactive():
@@ -558,13 +562,83 @@ def test_strict_work_counters():
     assert p.counters()["launches"] == 0
 
 
+def _oracle_strict_walk(job):
+    """Spawned worker: oracle.rollout_strict of one shared-CoP scenario (1 BLAS thread)."""
+    zx, zn, kick, n = job
+    from threadpoolctl import threadpool_limits
+    with threadpool_limits(1):
+        return O.rollout_strict(np.zeros(3), np.zeros(3), zx, zn, 150, 1.5 / 150, H, G, Q, R,
+                                kick=kick, kick_step=n // 2)
+
+
+def test_strict_shared_cop_config4():
+    """BASELINE config 4 (run_compare_resistance.py:87-169 scaled up): one shared default.json
+    CoP for every scenario (bounds stride 0: strict_lq.hip stages one group's lanes for the
+    whole launch and keeps cached checkpoints), x0 = 0, F_ext ~ U(0, 800) N, B = 4096.
+    The F = 0/400/800 N scenarios equal the reference-driven strict rollouts
+    (strict_ref.npz); 8 more scenarios equal the oracle's rollout; the x axis (no kick) is
+    the same for every scenario."""
+    import multiprocessing
+    from concurrent.futures import ProcessPoolExecutor
+    d = golden("strict_ref.npz")
+    zx, zn = d["n150_zmax"], d["n150_zmin"]
+    n, dt = len(zx), 1.5 / 150
+    B = 4096
+    F = np.random.default_rng(404).uniform(0.0, 800.0, B)
+    F[0], F[1], F[2] = 400.0, 0.0, 800.0
+    kick = dt * F / M
+    p = plan(150, strict=True)
+    hist, st = p.rollout(zx, zn, np.zeros((B, 2, 3)), kick=kick, kick_step=n // 2)
+    assert int(st.abs().max()) == 0
+    h = hist.cpu().numpy()
+    for b, Fv in ((0, 400), (1, 0), (2, 800)):
+        assert rmse(h[b, :, :, 0], d[f"n150_F{Fv}_com"]) <= 1e-9, Fv
+        assert rmse(h[b, :, 1] @ np.array([1.0, 0.0, -H / G]),
+                    d[f"n150_F{Fv}_yhist"] @ np.array([1.0, 0.0, -H / G])) <= 1e-9, Fv
+    pick = (3, 17, 500, 1023, 2048, 3001, 4000, 4095)
+    with ProcessPoolExecutor(max_workers=len(pick),
+                             mp_context=multiprocessing.get_context("spawn")) as ex:
+        refs = list(ex.map(_oracle_strict_walk, [(zx, zn, kick[b], n) for b in pick]))
+    for b, ref in zip(pick, refs):
+        assert rmse(h[b, :, :, 0], ref[:, :, 0]) <= 1e-9, b
+    assert np.abs(h[:, :, 0] - h[0:1, :, 0]).max() <= 1e-12
+
+
+def test_strict_shared_cop_full_size_properties():
+    """Config 4 at its full per-GPU size (125 000 scenarios, shared CoP): every scenario's
+    status is 0, the x-axis rows are the same for every scenario, and translating the CoP
+    and the initial CoM by δ translates every CoM position by δ."""
+    d = golden("strict_ref.npz")
+    zx, zn = d["n150_zmax"], d["n150_zmin"]
+    n, dt = len(zx), 1.5 / 150
+    B = 125_000
+    F = np.random.default_rng(405).uniform(0.0, 800.0, B)
+    kick = torch.as_tensor(dt * F / M, device="cuda")
+    p = plan(150, strict=True)
+    x0 = torch.zeros((B, 2, 3), dtype=torch.float64, device="cuda")
+    h1, s1 = p.rollout(zx, zn, x0, kick=kick, kick_step=n // 2)
+    delta = 0.0625
+    x1 = x0.clone()
+    x1[:, :, 0] += delta
+    h2, s2 = p.rollout(zx + delta, zn + delta, x1, kick=kick, kick_step=n // 2)
+    assert int(s1.abs().max()) == 0 and int(s2.abs().max()) == 0
+    assert float((h1[:, :, 0] - h1[0:1, :, 0]).abs().max()) <= 1e-12
+    assert float(((h2 - h1)[..., 0] - delta).abs().max()) <= 1e-7
+    assert float((h2 - h1)[..., 1:].abs().max()) <= 1e-5
+    # scenario 0 against the oracle (spot check inside the full-size launch)
+    ref = O.rollout_strict(np.zeros(3), np.zeros(3), zx, zn, 150, dt, H, G, Q, R,
+                           kick=float(kick[0]), kick_step=n // 2)
+    assert rmse(h1[0, :, :, 0].cpu().numpy(), ref[:, :, 0]) <= 1e-9
+
+
 # ------------------------------------------------ strict: long horizons, Cholesky cross-check
 
 
 def test_strict_long_horizon_rollout_vs_oracle():
     """N = 400: the LQ kernel with 4 waves per workgroup (8 waves' slot flags exceed LDS);
-    300 samples of the stepping phase, 800 N kick (tests/golden/strict_long_oracle.npz)."""
-    d = golden("strict_long_oracle.npz")
+    300 samples of the stepping phase, 800 N kick, vs the reference-driven strict rollout
+    (tests/golden/strict_long_ref.npz)."""
+    d = golden("strict_long_ref.npz")
     N = 400
     zx, zn = d["n400_zmax"], d["n400_zmin"]
     n = len(zx)
@@ -573,15 +647,15 @@ def test_strict_long_horizon_rollout_vs_oracle():
     hist, st = p.rollout(zx, zn, x0, kick=np.array([float(d["n400_kick"])]), kick_step=n // 2)
     assert int(st.abs().max()) == 0
     h = hist.cpu().numpy()[0]
-    ref = d["n400_hist"]
-    assert rmse(h[:, :, 0], ref[:, :, 0]) <= 1e-9
-    assert np.abs(h - ref).max() <= 1e-6
+    assert rmse(h[:, :, 0], d["n400_com"]) <= 1e-9
+    assert np.abs(h[:, 1] - d["n400_yhist"]).max() <= 1e-6
 
 
 @pytest.mark.parametrize("N", (400, 700, 1300))
 def test_strict_long_horizon_step_vs_oracle(N):
-    """Cold-start strict solves at horizons run with 4, 2 and 1 waves per workgroup."""
-    d = golden("strict_long_oracle.npz")
+    """Cold-start strict solves at horizons run with 4, 2 and 1 waves per workgroup, vs the
+    reference's own strict calls (strict_long_ref.npz)."""
+    d = golden("strict_long_ref.npz")
     p = plan(N, strict=True)
     out, st = p.step(d[f"step{N}_x"], d[f"step{N}_zmax"], d[f"step{N}_zmin"])
     ref = d[f"step{N}_out"]
@@ -609,7 +683,7 @@ for N in (64, 150):
         h, st = p.rollout(zx, zn, np.zeros((1, 2, 3)), kick=np.array([dt * F / 40.0]),
                           kick_step=n // 2)
         assert int(st.abs().max()) == 0
-        errs[f"n{N}_F{F}"] = rmse(h.cpu().numpy()[0][:, :, 0], s[f"n{N}_F{F}_hist"][:, :, 0])
+        errs[f"n{N}_F{F}"] = rmse(h.cpu().numpy()[0][:, :, 0], s[f"n{N}_F{F}_com"])
     out, st = p.step(s[f"step{N}_x"], s[f"step{N}_zmax"], s[f"step{N}_zmin"])
     ref = s[f"step{N}_out"]
     errs[f"step{N}"] = float(np.abs(out.cpu().numpy() - ref).max() / max(1.0, np.abs(ref).max()))
@@ -618,7 +692,7 @@ zx, zn = l["n400_zmax"], l["n400_zmin"]; n = len(zx)
 x0 = np.stack([l["n400_x0"], l["n400_y0"]])[None]
 h, st = p.rollout(zx, zn, x0, kick=np.array([float(l["n400_kick"])]), kick_step=n // 2)
 assert int(st.abs().max()) == 0
-errs["n400"] = rmse(h.cpu().numpy()[0][:, :, 0], l["n400_hist"][:, :, 0])
+errs["n400"] = rmse(h.cpu().numpy()[0][:, :, 0], l["n400_com"])
 out, st = p.step(l["step400_x"], l["step400_zmax"], l["step400_zmin"])
 ref = l["step400_out"]
 errs["step400"] = float(np.abs(out.cpu().numpy() - ref).max() / max(1.0, np.abs(ref).max()))
@@ -637,9 +711,9 @@ def test_strict_cholesky_variant_vs_oracle():
     import sys
     env = dict(os.environ, ZMPC_STRICT_VARIANT="chol")
     r = subprocess.run([sys.executable, "-c", _CHOL_CHILD, PKG,
-                        os.path.join(os.path.dirname(__file__), "golden", "strict_oracle.npz"),
+                        os.path.join(os.path.dirname(__file__), "golden", "strict_ref.npz"),
                         os.path.join(os.path.dirname(__file__), "golden",
-                                     "strict_long_oracle.npz")],
+                                     "strict_long_ref.npz")],
                        env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0 and "CHOL_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
 
