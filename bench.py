@@ -28,6 +28,8 @@ Prints ONE JSON line (rank 0).
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -44,7 +46,7 @@ for _p in (ROOT, PKG):
 from mpc_bipedal.config import MPCConfig  # noqa: E402
 from mpc_bipedal.generators import CoPGenerator  # noqa: E402
 from mpc_bipedal.solver import Plan  # noqa: E402
-from mpc_bipedal.distributed import allgather_walks  # noqa: E402
+from mpc_bipedal.distributed import allgather_walks, shard_range  # noqa: E402
 
 # configs/default.json "mpc" section of the reference (the fields the CoP producer and the
 # Wieber hot path read)
@@ -137,32 +139,16 @@ def herdt_bench(args, rank, world, dev):
     x0 = torch.as_tensor(x0_h, device=dev)
     kick = torch.as_tensor(kick_h, device=dev)
 
+    last = {}
+
     def launch():
-        return plan.herdt_rollout(prm, v, s_t, nb_t, x0, kick=kick, kick_step=n // 2)
+        last["out"] = plan.herdt_rollout(prm, v, s_t, nb_t, x0, kick=kick, kick_step=n // 2)
     for _ in range(args.warmup):
         launch()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    stream = torch.cuda.current_stream()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     plan.counters(reset=True)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
-        hist, foot, status = launch()
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        dist.barrier()
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    kern_ms = ev0.elapsed_time(ev1) / args.steps
+    elapsed, kern_ms = timed_region(launch, args.steps, world, dev)
     cnt = plan.counters(reset=True)
+    hist, foot, status = last["out"]
     assert int(status.abs().max()) == 0, "solver reported a failed instance"
     solves_per_step = B * (n - 1) * world
     value = solves_per_step * args.steps / elapsed
@@ -427,6 +413,243 @@ def pmc_traffic(workload):
         return None
 
 
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(gpus, argv):
+    """`bench.py --gpus N` without a launcher around it: start N ranks of this script (one
+    process per GPU, RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* as torchrun sets them, rendezvous on
+    127.0.0.1) and wait for them.  The parent never touches the GPU; it returns the first
+    non-zero exit code, and stops the other ranks when one fails (they would wait in a
+    collective forever)."""
+    port = _free_port()
+    procs = []
+    for r in range(gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(gpus),
+                   LOCAL_WORLD_SIZE=str(gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv,
+                                      env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def timed_region(launch, steps, world, dev):
+    """The bench contract's timed region: barrier + sync on both sides of exactly `steps`
+    launches, the job time = max over ranks.  Returns (elapsed seconds, average launch duration
+    in ms from one HIP event pair on the launch stream — None on CPU)."""
+    cuda = dev.type == "cuda"
+    sync = torch.cuda.synchronize if cuda else (lambda: None)
+    sync()
+    if world > 1:
+        dist.barrier()
+    sync()
+    if cuda:
+        # one event pair brackets the K back-to-back launches on their stream (per-launch
+        # pairs would add a marker packet, and an idle gap, between consecutive kernels)
+        stream = torch.cuda.current_stream()
+        ev0 = torch.cuda.Event(enable_timing=True)
+        ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    if cuda:
+        ev0.record(stream)
+    for _ in range(steps):
+        launch()
+    if cuda:
+        ev1.record(stream)
+    sync()
+    # this rank's time from the common start to its last launch finishing; the job time is the
+    # max over ranks, so the closing barrier's own latency is not charged
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device=dev if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, (ev0.elapsed_time(ev1) / steps if cuda else None)
+
+
+def gather_com(com, total, world, dev):
+    """All-gather of the per-rank CoM blocks (RCCL over xGMI on GPUs): (full [total, ...],
+    milliseconds), timed separately from `value`."""
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    dist.barrier()
+    tg = time.perf_counter()
+    if dist.get_backend() != "nccl":
+        com = com.cpu()  # gloo rehearsal: host buffers
+    full = allgather_walks(com, total)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    return full, (time.perf_counter() - tg) * 1e3
+
+
+def stub_bench(args, rank, world):
+    """`--stub-solver`: the multi-rank plumbing of this script on CPU (gloo) with a stand-in
+    per-rank solver — spawn → shard → timed region → all-gather → one JSON line — for the CPU
+    test of the launcher (tests/test_distributed.py).  Walk w's "history" is w + t/1000 at
+    timestep t, so the reassembled batch proves every shard landed in its place."""
+    B = args.batch or 8
+    n = 16
+    dev = torch.device("cpu")
+    total = B * world
+    a, b = shard_range(total, world, rank)
+    idx = torch.arange(a, b, dtype=torch.float64)[:, None]
+    hist = torch.empty((b - a, n, 2, 3), dtype=torch.float64)
+
+    def launch():
+        hist[:] = (idx + torch.arange(n, dtype=torch.float64)[None] / 1000.0)[..., None, None]
+    for _ in range(args.warmup):
+        launch()
+    elapsed, _ = timed_region(launch, args.steps, world, dev)
+    full, gather_ms = gather_com(hist[..., 0].contiguous(), total, world, dev)
+    expect = (torch.arange(total, dtype=torch.float64)[:, None] +
+              torch.arange(n, dtype=torch.float64)[None] / 1000.0)[..., None]
+    ok = bool(torch.equal(full, expect.expand(total, n, 2)))
+    if rank == 0:
+        print(json.dumps({
+            "metric": "launcher self-test (stub solver)", "value": total * (n - 1) * 2 *
+            args.steps / elapsed, "unit": "stub solves/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3,
+            "scaling": "weak", "world_size": dist.get_world_size(), "backend": "gloo",
+            "config": {"walks_per_gpu": B, "global_batch": total, "parallelism": f"dp{world}"},
+            "allgather_ms": gather_ms, "gather_ok": ok}))
+    return ok
+
+
+def harness_cpu_seconds(N, strict, n_steps=100):
+    """The reference's own perf harness, run_compare_runtime.py:21-73, on the CPU port: a
+    controller for MPCConfig(horizon=N, strict=..., add_force=False), dummy ±0.1 m bounds over
+    n_steps samples padded by the horizon (:21-33), `_run_once` = one x-axis and one y-axis
+    predict_wieber_axis on the window [1:1+N] (= 2 QP solves, :44-57), 3 warm-up calls, then
+    the MEAN of 10 timed calls from a zero state (:59-73).  The port: oracle
+    predict_wieber_axis_ref (interpreted Px/Pu loop + np.linalg.inv, zmp_controller.py:162-199);
+    strict: the same loop build + the exact box-QP (the reference's cvxpy/OSQP is absent).
+    Returns seconds per `_run_once`."""
+    from oracle import zmp_oracle as O
+    cfg = MPCConfig(horizon=N, strict=strict, add_force=False)
+    zmax = np.vstack([np.ones((n_steps, 2)) * 0.1, np.ones((N, 2)) * 0.1])
+    zmin = -zmax
+    hi = zmax[1:1 + N]
+    lo = zmin[1:1 + N]
+
+    def axis(x, a):
+        if not strict:
+            return O.predict_wieber_axis_ref(x, N, hi[:, a:a + 1], lo[:, a:a + 1], cfg.dt, cfg.h,
+                                             cfg.g, cfg.Q, cfg.R)
+        A, Bv, _ = O.lipm(cfg.dt, cfg.h, cfg.g)
+        Px, Pu = O.prediction_matrices_loop(N, cfg.dt, cfg.h, cfg.g)   # :162-171 per call
+        V = np.linalg.solve(Pu, np.eye(N))
+        Hz = cfg.Q * np.eye(N) + cfg.R * V.T @ V
+        u0, _, _, _ = O.strict_u0(x.ravel(), hi[:, a], lo[:, a], Hz, Px, Pu[0, 0], cfg.Q)
+        return A @ x + Bv * u0
+
+    def run_once(x, y):
+        return axis(x, 0), axis(y, 1)
+    x, y = np.zeros((3, 1)), np.zeros((3, 1))
+    for _ in range(3):
+        x, y = run_once(x, y)
+    times = []
+    for _ in range(10):
+        x, y = np.zeros((3, 1)), np.zeros((3, 1))
+        t0 = time.perf_counter()
+        run_once(x, y)
+        times.append(time.perf_counter() - t0)
+    return float(np.mean(times))
+
+
+def sweep_horizon(args, dev):
+    """`--sweep-horizon`: the reference harness's horizon sweep (run_compare_runtime.py:139,
+    N = 10..300 step 10) on both sides, one JSON line per horizon plus a summary line.
+      gpu_batched: B default.json walks (CoP at that horizon, dt = 1.5/N, rigid offsets as
+        config 2) rolled out per launch — QP solves/s, inputs resident in HBM, HIP-event
+        timed; unconstrained and strict;
+      gpu_call_ms: the harness's own semantics on the drop-in (ZMPController.predict_wieber_axis
+        with host NumPy arrays: H2D, one kernel, D2H) — mean of 10 `_run_once` after 3 warm-ups;
+      cpu_call_ms: the same harness on the CPU port (harness_cpu_seconds), 1 process, 1 BLAS
+        thread."""
+    from threadpoolctl import threadpool_limits
+    from mpc_bipedal.controllers import ZMPController
+    lo, hi, step = (int(v) for v in args.sweep_horizon.split(":"))
+    Bu = args.batch or 4096
+    Bs = max(64, Bu // 4)
+    rows = []
+    for N in range(lo, hi + 1, step):
+        row = {"N": N}
+        for strict in (False, True):
+            d = dict(DEFAULT_JSON, horizon=N, strict=strict)
+            cfg = MPCConfig(**d)
+            B = Bs if strict else Bu
+            _, _, zmax_h, zmin_h, x0_h, F_h = make_batch(B, 0, cfg, False)
+            n = zmax_h.shape[1]
+            plan = Plan(dev.index, N, cfg.dt, cfg.h, cfg.g, cfg.Q, cfg.R, strict)
+            zmax = torch.as_tensor(zmax_h, device=dev)
+            zmin = torch.as_tensor(zmin_h, device=dev)
+            x0 = torch.as_tensor(x0_h, device=dev)
+            kick = torch.as_tensor(cfg.dt * F_h / cfg.m, device=dev)
+            launch = plan.rollout_launcher(zmax, zmin, x0, kick=kick, kick_step=n // 2)
+            launch()
+            steps = 3 if strict else 10
+            elapsed, kern_ms = timed_region(launch, steps, 1, dev)
+            assert int(launch.status.abs().max()) == 0
+            tag = "strict" if strict else "unc"
+            row[f"gpu_batched_{tag}"] = B * (n - 1) * 2 * steps / elapsed
+            row[f"kernel_ms_{tag}"] = kern_ms
+            row[f"walks_{tag}"] = B
+            row["samples_per_walk"] = n
+            row[f"plan_build_ms_{tag}"] = plan.timings()["total"]
+            # the harness on the drop-in (host arrays in and out, one solve pair per call)
+            c = ZMPController(MPCConfig(horizon=N, strict=strict, add_force=False))
+            zx = np.ones((N, 1)) * 0.1
+            zn = -zx
+
+            def run_once(x, y):
+                return (c.predict_wieber_axis(x, N, zx, zn), c.predict_wieber_axis(y, N, zx, zn))
+            xs, ys = np.zeros((3, 1)), np.zeros((3, 1))
+            for _ in range(3):
+                xs, ys = run_once(xs, ys)
+            ts = []
+            for _ in range(10):
+                t0 = time.perf_counter()
+                run_once(np.zeros((3, 1)), np.zeros((3, 1)))
+                ts.append(time.perf_counter() - t0)
+            row[f"gpu_call_ms_{tag}"] = float(np.mean(ts)) * 1e3
+            if not args.no_cpu_baseline:
+                with threadpool_limits(1):
+                    row[f"cpu_call_ms_{tag}"] = harness_cpu_seconds(N, strict) * 1e3
+                row[f"cpu_solves_per_s_{tag}"] = 2.0 / (row[f"cpu_call_ms_{tag}"] * 1e-3)
+            plan.destroy()
+        print(json.dumps(row), flush=True)
+        rows.append(row)
+    print(json.dumps({
+        "metric": "horizon sweep (run_compare_runtime.py:139 semantics): QP solves/s vs N",
+        "unit": "QP solves/s", "n_gpus": 1, "dtype": "f64", "cpu_cores": 1,
+        "horizons": [r["N"] for r in rows],
+        "gpu_batched_unc": [r["gpu_batched_unc"] for r in rows],
+        "gpu_batched_strict": [r["gpu_batched_strict"] for r in rows],
+        "cpu_solves_per_s_unc": [r.get("cpu_solves_per_s_unc") for r in rows],
+        "cpu_solves_per_s_strict": [r.get("cpu_solves_per_s_strict") for r in rows],
+        "config": {"walks_unc": Bu, "walks_strict": Bs, "workload": "default.json walks at each "
+                   "horizon (dt = 1.5/N) + rigid offsets, F_ext ~ U(0, 800) N"}}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -440,21 +663,57 @@ def main():
     ap.add_argument("--unconstrained", action="store_true", help="config 4 unconstrained variant")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only to "
+                         "rehearse several ranks on fewer GPUs)")
+    ap.add_argument("--sweep-horizon", default=None, metavar="LO:HI:STEP",
+                    help="horizon sweep of the reference harness (e.g. 10:300:10), "
+                         "run_compare_runtime.py:139; prints one line per horizon")
+    ap.add_argument("--stub-solver", action="store_true",
+                    help="CPU/gloo self-test of the multi-rank launcher (no GPU, no solver)")
     ap.add_argument("--pipelined", action="store_true",
                     help="also time batches pipelined two-deep on two streams (reported beside "
                          "value; off by default so a profile of the default command sees only "
                          "non-overlapped launches)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # no launcher around us (the driver's torchrun form sets WORLD_SIZE): start the ranks
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.stub_solver:
+        if world > 1:
+            dist.init_process_group("gloo")
+            assert dist.get_world_size() == args.gpus
+        ok = stub_bench(args, rank, world)
+        if world > 1:
+            dist.destroy_process_group()
+        sys.exit(0 if ok else 1)
     if world > 1:
+        ndev = torch.cuda.device_count()
+        if local >= ndev and args.dist_backend == "nccl":
+            raise SystemExit(f"rank {rank}: LOCAL_RANK {local} but only {ndev} GPU(s) visible")
+        local %= ndev  # gloo rehearsal may put several ranks on one GPU
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
+        assert dist.get_world_size() == args.gpus
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
+    if args.sweep_horizon:
+        if world > 1:
+            raise SystemExit("--sweep-horizon runs on one GPU")
+        sweep_horizon(args, dev)
+        return
 
     conf = 3 if args.strict else args.config
     if CONFIGS[conf].get("herdt"):
@@ -491,33 +750,8 @@ def main():
     torch.cuda.synchronize()
     if cfg.strict:
         plan.counters(reset=True)  # count the timed launches only
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    stream = torch.cuda.current_stream()
-    # one HIP event pair brackets the K back-to-back launches on their stream: kernel_ms is
-    # the average launch duration (per-launch event pairs would add a marker packet, and an
-    # idle gap, between consecutive kernels)
-    ev0 = torch.cuda.Event(enable_timing=True)
-    ev1 = torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for k in range(args.steps):
-        launch()
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    # this rank's time from the common start to its last launch finishing; the job time is
-    # the max over ranks (below), so the closing barrier's own latency is not charged
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    kern_ms = ev0.elapsed_time(ev1) / args.steps
+    elapsed, kern_ms = timed_region(launch, args.steps, world, dev)
     work = plan.counters() if cfg.strict else None
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
     assert int(status.abs().max()) == 0, "solver reported a failed instance"
 
     solves_per_step = B * (n - 1) * 2 * world
@@ -552,13 +786,7 @@ def main():
 
     gather_ms = None
     if world > 1:
-        com = hist[..., 0].contiguous()
-        torch.cuda.synchronize()
-        dist.barrier()
-        tg = time.perf_counter()
-        full = allgather_walks(com, B * world)
-        torch.cuda.synchronize()
-        gather_ms = (time.perf_counter() - tg) * 1e3
+        full, gather_ms = gather_com(hist[..., 0].contiguous(), B * world, world, dev)
         assert full.shape[0] == B * world
 
     # batches pipelined two-deep on two streams (separate history buffers): consecutive

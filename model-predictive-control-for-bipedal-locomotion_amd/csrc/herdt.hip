@@ -136,7 +136,9 @@ __device__ void polytope_segment(const double (*P)[3], int nfac, int i, double* 
 // unconstrained point when feasible, else the best clamped projection onto a facet segment
 // (the optimum of a convex QP outside its minimiser lies on the boundary: inside a facet, or
 // at a vertex = a segment end).
-__device__ void polytope_qp(const PolyLds& L, int sd, int nfac, double sx, double sy, double ux,
+// Returns false when the point is outside and no facet segment is usable (a degenerate or
+// unbounded polygon through the C-ABI): the caller flags the walk (ZMPC_ST_INFEASIBLE).
+__device__ bool polytope_qp(const PolyLds& L, int sd, int nfac, double sx, double sy, double ux,
                             double uy, double* dx, double* dy) {
   const double tol = 1e-12;
   bool inside = true;
@@ -145,12 +147,14 @@ __device__ void polytope_qp(const PolyLds& L, int sd, int nfac, double sx, doubl
   if (inside) {
     *dx = ux;
     *dy = uy;
-    return;
+    return true;
   }
   double best = 1e300, bx = ux, by = uy;
+  bool any = false;
   for (int i = 0; i < nfac; ++i) {
     const double* e = L.seg[sd][i];
     if (isnan(e[0])) continue;
+    any = true;
     const double wx = e[2] - e[0], wy = e[3] - e[1];
     const double rx = e[0] - ux, ry = e[1] - uy;
     const double den = sx * wx * wx + sy * wy * wy;
@@ -166,6 +170,7 @@ __device__ void polytope_qp(const PolyLds& L, int sd, int nfac, double sx, doubl
   }
   *dx = bx;
   *dy = by;
+  return any;
 }
 
 // Cholesky factor of the M×M footstep block F of P (packed, NA-indexed at offset 3): L lower,
@@ -502,7 +507,10 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
     mw = __builtin_amdgcn_readfirstlane(mw);
     const int M = m - ((m > 0 && lastbreak == N - 1) ? 1 : 0);  // with rows in the horizon
     const bool stand_mode = (cur == ZMPC_STANDING || nstand == N) && nstand > 0;
-    if (m > MM) fq |= ZMPC_ST_FACTOR;  // host sizes MM from the batch; never expected
+    // host sizes MM from the batch; never expected.  Sweep 1 runs at the wave's largest count,
+    // clamped to MM, so a wave holding any such lane solves a truncated problem for every
+    // lane: flag them all (mw is wave-uniform), no walk reports success from it
+    if (mw > MM) fq |= ZMPC_ST_FACTOR;
     // standing bounds (:721-744)
     double slo = 0.0, shi = 0.0;
     {
@@ -602,7 +610,8 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
           const double ux = __shfl(uu, lane & ~1, 64), uy = __shfl(uu, lane | 1, 64);
           const double fcx = __shfl(fc, lane & ~1, 64), fcy = __shfl(fc, lane | 1, 64);
           double dx, dy;
-          polytope_qp(pl, side, nfac, sx, sy, ux - fcx, uy - fcy, &dx, &dy);
+          if (!polytope_qp(pl, side, nfac, sx, sy, ux - fcx, uy - fcy, &dx, &dy))
+            fq |= ZMPC_ST_INFEASIBLE;
           fx0 = axis ? fcy + dy : fcx + dx;
         }
         // the other footsteps minimise V_0 with f0 fixed: the KKT point of F f − g = μ e₀ is
@@ -619,13 +628,13 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
       };
       switch (mw) {
         case 0: sweep1(std::integral_constant<int, 3>{}); break;
-        case 1: sweep1(std::integral_constant<int, (MM >= 1 ? 4 : 3)>{}); break;
-        case 2: sweep1(std::integral_constant<int, (MM >= 2 ? 5 : 3)>{}); break;
-        case 3: sweep1(std::integral_constant<int, (MM >= 3 ? 6 : 3)>{}); break;
-        case 4: sweep1(std::integral_constant<int, (MM >= 4 ? 7 : 3)>{}); break;
-        case 5: sweep1(std::integral_constant<int, (MM >= 5 ? 8 : 3)>{}); break;
-        case 6: sweep1(std::integral_constant<int, (MM >= 6 ? 9 : 3)>{}); break;
-        case 7: sweep1(std::integral_constant<int, (MM >= 7 ? 10 : 3)>{}); break;
+        case 1: sweep1(std::integral_constant<int, 3 + (1 <= MM ? 1 : MM)>{}); break;
+        case 2: sweep1(std::integral_constant<int, 3 + (2 <= MM ? 2 : MM)>{}); break;
+        case 3: sweep1(std::integral_constant<int, 3 + (3 <= MM ? 3 : MM)>{}); break;
+        case 4: sweep1(std::integral_constant<int, 3 + (4 <= MM ? 4 : MM)>{}); break;
+        case 5: sweep1(std::integral_constant<int, 3 + (5 <= MM ? 5 : MM)>{}); break;
+        case 6: sweep1(std::integral_constant<int, 3 + (6 <= MM ? 6 : MM)>{}); break;
+        case 7: sweep1(std::integral_constant<int, 3 + (7 <= MM ? 7 : MM)>{}); break;
         default: sweep1(std::integral_constant<int, 3 + MM>{}); break;
       }
       // rows past the wave's last pinned row (the free tail) take K from ktab; the slab keeps

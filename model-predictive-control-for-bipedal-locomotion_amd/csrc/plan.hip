@@ -5,7 +5,7 @@
 // only on (N, dt, h, g, Q, R), so it is built once per plan here, on the device:
 //   1. p (Toeplitz column of Pu) and Px               zmp_controller.py:166-171
 //   2. M = PuᵀPu + (R/Q)·I  — FP64 MFMA at N >= 64     zmp_controller.py:198
-//   3. M = L Lᵀ (Cholesky)
+//   3. M = L Lᵀ (blocked Cholesky, 16-column panels, FP64 MFMA panel updates)
 //   4. y = M⁻¹ e0, gain row k = Pu y (= row 0 of inv(M) Puᵀ), kx = k·Px
 //   5. strict plans: X = L⁻¹ Puᵀ, G = XᵀX / Q = Pu (R·I + Q·PuᵀPu)⁻¹ Puᵀ,
 //      the inverse z-space Hessian of the strict QP (zmp_controller.py:173-195).
@@ -32,54 +32,69 @@ __global__ void zmpc_build_prediction(int N, double T, double T2_2, double T3_6,
 }
 
 // Operand fetchers for the Gram kernels: value of the (k, a) element of the matrix whose
-// columns are contracted, C[a][b] = Σ_k Op(k,a)·Op(k,b).
-struct PuOp {  // Pu[k][a] = p(k-a) for k >= a
-  const double* p;
-  int N;
-  __device__ double operator()(int k, int a) const {
-    return (k < N && a < N && k >= a) ? p[k - a] : 0.0;
-  }
-  __device__ int kbegin(int a0, int b0) const { return (a0 > b0 ? a0 : b0) & ~3; }
-};
+// columns are contracted, C[a][b] = Σ_k Op(k,a)·Op(k,b).  `stage` copies what the operand reads
+// into LDS once per workgroup (the Toeplitz column: N doubles) so the K loop reads LDS.
 struct ToeplitzOp {  // lower-triangular Toeplitz T[k][a] = c(k-a) for k >= a (Pu, or Pu⁻¹)
   const double* c;
   int N;
-  __device__ double operator()(int k, int a) const {
-    return (k < N && a < N && k >= a) ? c[k - a] : 0.0;
+  static constexpr bool kStaged = true;
+  __device__ double at(const double* sc, int k, int a) const {
+    return (k < N && a < N && k >= a) ? sc[k - a] : 0.0;
   }
   __device__ int kbegin(int a0, int b0) const { return (a0 > b0 ? a0 : b0) & ~3; }
 };
+using PuOp = ToeplitzOp;  // Pu[k][a] = p(k-a)
 struct DenseOp {  // X[k][a], row-major N×N
   const double* X;
   int N;
-  __device__ double operator()(int k, int a) const {
+  static constexpr bool kStaged = false;
+  __device__ double at(const double*, int k, int a) const {
     return (k < N && a < N) ? X[(size_t)k * N + a] : 0.0;
   }
   __device__ int kbegin(int, int) const { return 0; }
 };
 
-// 2/5. C = alpha·OpᵀOp + diag·I with v_mfma_f64_16x16x4_f64: one wave per 16×16 tile.
+// 2/5. C = alpha·OpᵀOp + diag·I with v_mfma_f64_16x16x4_f64: one wave per 16×16 tile of the
+// lower triangle (ta >= tb; C is symmetric, the tile is written to both halves), two
+// accumulators alternating so consecutive MFMAs do not wait on each other's result.
 // Operand lane map (gfx950): A[i = lane&15][k = lane>>4], B[k = lane>>4][j = lane&15];
 // result D: col = lane&15, row = (lane>>4) + 4·r.
 template <class Op>
 __global__ void __launch_bounds__(64) zmpc_gram_mfma(int N, Op op, double alpha, double diag,
                                                      double* __restrict__ C) {
-  const int tiles = (N + 15) >> 4;
-  const int ta = blockIdx.x / tiles, tb = blockIdx.x % tiles;
+  extern __shared__ double sc[];  // staged operand (Toeplitz column), N doubles
+  const int t = blockIdx.x;
+  int ta = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+  while ((ta + 1) * (ta + 2) / 2 <= t) ++ta;
+  while (ta * (ta + 1) / 2 > t) --ta;
+  const int tb = t - ta * (ta + 1) / 2;
   const int a0 = ta << 4, b0 = tb << 4;
   const int lane = threadIdx.x;
   const int r = lane & 15, kq = lane >> 4;
-  dbl4 acc = {0.0, 0.0, 0.0, 0.0};
-  for (int k0 = op.kbegin(a0, b0); k0 < N; k0 += 4) {
-    const int k = k0 + kq;
-    const double av = op(k, a0 + r);
-    const double bv = op(k, b0 + r);
-    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc, 0, 0, 0);
+  if constexpr (Op::kStaged) {
+    for (int j = lane; j < N; j += 64) sc[j] = op.c[j];
+    __syncthreads();
+  }
+  dbl4 acc0 = {0.0, 0.0, 0.0, 0.0}, acc1 = {0.0, 0.0, 0.0, 0.0};
+  int k0 = op.kbegin(a0, b0);
+  for (; k0 + 4 < N; k0 += 8) {
+    const double av0 = op.at(sc, k0 + kq, a0 + r), bv0 = op.at(sc, k0 + kq, b0 + r);
+    const double av1 = op.at(sc, k0 + 4 + kq, a0 + r), bv1 = op.at(sc, k0 + 4 + kq, b0 + r);
+    acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av0, bv0, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(av1, bv1, acc1, 0, 0, 0);
+  }
+  if (k0 < N) {
+    const double av = op.at(sc, k0 + kq, a0 + r), bv = op.at(sc, k0 + kq, b0 + r);
+    acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(av, bv, acc0, 0, 0, 0);
   }
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int a = a0 + kq + 4 * q, b = b0 + r;
-    if (a < N && b < N) C[(size_t)a * N + b] = alpha * acc[q] + (a == b ? diag : 0.0);
+    const double v = alpha * (acc0[q] + acc1[q]) + (a == b ? diag : 0.0);
+    if (a < N && b < N) {
+      C[(size_t)a * N + b] = v;
+      if (ta != tb) C[(size_t)b * N + a] = v;
+    }
   }
 }
 
@@ -90,72 +105,180 @@ __global__ void zmpc_gram_fma(int N, Op op, double alpha, double diag, double* _
   if (idx >= N * N) return;
   const int a = idx / N, b = idx % N;
   double s = 0.0;
-  for (int k = op.kbegin(a, b); k < N; ++k) s = fma(op(k, a), op(k, b), s);
+  const double* src = nullptr;
+  if constexpr (Op::kStaged) src = op.c;
+  for (int k = op.kbegin(a, b); k < N; ++k) s = fma(op.at(src, k, a), op.at(src, k, b), s);
   C[idx] = alpha * s + (a == b ? diag : 0.0);
 }
 
-// 3. Right-looking Cholesky of the N×N matrix in L (in place), one workgroup; the pivot
-// column is staged in LDS.  info = 0 on success, k+1 if the k-th pivot is not positive.
-__global__ void __launch_bounds__(1024) zmpc_cholesky(int N, double* __restrict__ L,
+// 3. Blocked left-looking Cholesky M = L Lᵀ (L written from M), 16-column panels, one launch per
+// panel p0 (p0 = 0, 16, 32, ...), one wave per 16-row tile of rows [p0, N).  Every wave
+//  (a) forms the panel's diagonal tile D = M[p0.., p0..] − L[p0.., :p0]·L[p0.., :p0]ᵀ and its own
+//      tile T = M[r0.., p0..] − L[r0.., :p0]·L[p0.., :p0]ᵀ with v_mfma_f64_16x16x4_f64 (K = p0,
+//      the L rows streamed 16 columns per batch, loads issued ahead of the MFMAs),
+//  (b) factors D = Lpp·Lppᵀ in registers (lane i holds row i; columns broadcast by shuffles),
+//  (c) solves its tile, L[r0.., p0..] = T·Lpp⁻ᵀ (lane i owns row i),
+// and wave 0 writes Lpp and zeroes the upper triangle of its 16 rows.  The M entries come from
+// M itself, never from L: wave 0 overwrites the diagonal block in L while the other waves of the
+// launch may still be reading it.  Every entry of L is written by some panel (lower part as
+// Lpp / T, upper part zeroed), so L needs no initial copy of M.
+// info = 0 on success, else the first non-positive pivot's index + 1.
+__global__ void __launch_bounds__(64) zmpc_chol_panel(int N, int p0, const double* __restrict__ M,
+                                                      double* __restrict__ L,
                                                       int* __restrict__ info) {
-  extern __shared__ double col[];  // [N]
-  __shared__ int bad;
-  const int tid = threadIdx.x, nt = blockDim.x;
-  if (tid == 0) bad = 0;
-  __syncthreads();
-  for (int k = 0; k < N; ++k) {
-    const double d = L[(size_t)k * N + k];
-    if (!(d > 0.0)) {
-      if (tid == 0) { bad = k + 1; }
-      break;
+  __shared__ double sD[16][17];
+  __shared__ double sT[16][17];
+  const int lane = threadIdx.x, r = lane & 15, kq = lane >> 4;
+  const int r0 = p0 + 16 * blockIdx.x;
+  const bool diag = blockIdx.x == 0;
+  const int pr = p0 + r, tr = r0 + r;
+  const bool pok = pr < N, tok = tr < N;
+  const double* Lp = L + (size_t)(pok ? pr : 0) * N;
+  const double* Lt = L + (size_t)(tok ? tr : 0) * N;
+  dbl4 accD = {0.0, 0.0, 0.0, 0.0}, accT = {0.0, 0.0, 0.0, 0.0};
+  // k = k0 + 4·kq + u: each lane reads 4 consecutive doubles of its row per batch; A and B of
+  // one MFMA step come from the same (kq, u), so the contraction runs over every k < p0 once
+  for (int k0 = 0; k0 < p0; k0 += 16) {
+    double a[4], b[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int k = k0 + 4 * kq + u;
+      a[u] = pok ? Lp[k] : 0.0;
+      b[u] = (!diag && tok) ? Lt[k] : 0.0;
     }
-    const double piv = sqrt(d);
-    for (int i = k + tid; i < N; i += nt) {
-      const double v = (i == k) ? piv : L[(size_t)i * N + k] / piv;
-      col[i] = v;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      accD = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u], a[u], accD, 0, 0, 0);
+      if (!diag) accT = __builtin_amdgcn_mfma_f64_16x16x4f64(b[u], a[u], accT, 0, 0, 0);
     }
-    __syncthreads();
-    for (int i = k + tid; i < N; i += nt) L[(size_t)i * N + k] = col[i];
-    const int m = N - k - 1;
-    for (int idx = tid; idx < m * m; idx += nt) {
-      const int i = k + 1 + idx / m, j = k + 1 + idx % m;
-      if (j <= i) L[(size_t)i * N + j] -= col[i] * col[j];
+  }
+  // acc[q] = (row kq + 4q, column r) of the product; subtract from M (identity padding past N)
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int i = kq + 4 * q;
+    const bool inD = (p0 + i < N) && pok;
+    sD[i][r] = inD ? M[(size_t)(p0 + i) * N + pr] - accD[q] : (i == r ? 1.0 : 0.0);
+    if (!diag) {
+      const bool inT = (r0 + i < N) && pok;
+      sT[i][r] = inT ? M[(size_t)(r0 + i) * N + pr] - accT[q] : 0.0;
     }
-    __syncthreads();
   }
   __syncthreads();
-  for (int idx = tid; idx < N * N; idx += nt) {
-    const int i = idx / N, j = idx % N;
-    if (j > i) L[idx] = 0.0;
+  // (b) 16×16 Cholesky, lane r holds row r of D (every lane group of 16 computes the same)
+  double d[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) d[c] = sD[r][c];
+  int bad = 0;
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    const double dc = __shfl(d[c], c, 64);
+    if (!(dc > 0.0) && bad == 0) bad = c + 1;
+    const double piv = sqrt(dc);
+    const double l = (r == c) ? piv : d[c] / piv;  // L[r][c] for r >= c
+    d[c] = (r >= c) ? l : 0.0;
+#pragma unroll
+    for (int j = c + 1; j < 16; ++j) {
+      const double ljc = __shfl(l, j, 64);
+      if (r >= j) d[j] = fma(-l, ljc, d[j]);
+    }
   }
-  if (tid == 0) *info = bad;
+  if (diag) {
+    if (kq == 0 && pok) {
+#pragma unroll
+      for (int c = 0; c < 16; ++c)
+        if (p0 + c < N) L[(size_t)pr * N + p0 + c] = d[c];
+    }
+    if (pok)
+      for (int j = p0 + 16 + kq; j < N; j += 4) L[(size_t)pr * N + j] = 0.0;
+    if (lane == 0 && bad != 0 && *info == 0) *info = p0 + bad;
+    return;
+  }
+  // (c) X·Lppᵀ = T row by row: X[r][c] = (T[r][c] − Σ_{m<c} X[r][m]·Lpp[c][m]) / Lpp[c][c]
+  double t[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) t[c] = sT[r][c];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    double acc = t[c];
+#pragma unroll
+    for (int m = 0; m < c; ++m) acc = fma(-t[m], __shfl(d[m], c, 64), acc);
+    t[c] = acc / __shfl(d[c], c, 64);
+  }
+  if (kq == 0 && tok) {
+#pragma unroll
+    for (int c = 0; c < 16; ++c)
+      if (p0 + c < N) L[(size_t)tr * N + p0 + c] = t[c];
+  }
 }
 
-// 4. y = M⁻¹ e0 by two triangular solves in LDS, k = Pu y, kx = k·Px.  One workgroup.
+// 4. y = M⁻¹ e0 by two blocked triangular solves (64-row blocks), then k = Pu y, kx = k·Px.
+// One 1024-thread workgroup.  Per block: the off-block part of every row's dot product is a
+// wave reduction over coalesced row (forward) / column-block (backward) reads, the 64×64
+// diagonal block is staged in LDS and solved by wave 0 with shuffles — two barriers per block
+// instead of two per column.
 __global__ void __launch_bounds__(1024) zmpc_gain(int N, int Kpad, const double* __restrict__ L,
                                                   const double* __restrict__ p,
                                                   const double* __restrict__ Px,
                                                   double* __restrict__ k,
                                                   double* __restrict__ kx) {
-  extern __shared__ double w[];  // [N]
+  extern __shared__ double w[];             // [N]
+  __shared__ double blk[64][65];            // diagonal block
+  __shared__ double part[16][64];           // partial sums
   __shared__ double red[3][1024 / 64];
-  const int tid = threadIdx.x, nt = blockDim.x;
-  for (int i = tid; i < N; i += nt) w[i] = (i == 0) ? 1.0 : 0.0;
-  __syncthreads();
-  // forward: L w = e0 (column-oriented)
-  for (int j = 0; j < N; ++j) {
-    const double wj = w[j] / L[(size_t)j * N + j];
+  const int tid = threadIdx.x, nt = blockDim.x, lane = tid & 63, wv = tid >> 6;
+  // forward: L w = e0
+  for (int b0 = 0; b0 < N; b0 += 64) {
+    const int nb = min(64, N - b0);
+    for (int idx = tid; idx < 64 * 64; idx += nt) {
+      const int i = idx >> 6, c = idx & 63;
+      blk[i][c] = (i < nb && c < nb) ? L[(size_t)(b0 + i) * N + b0 + c] : 0.0;
+    }
+    // t_i = Σ_{c<b0} L[b0+i][c] w[c]: wave wv takes rows wv, wv+16, ...; lanes over c
+    for (int i = wv; i < nb; i += 16) {
+      double s = 0.0;
+      const double* row = L + (size_t)(b0 + i) * N;
+      for (int c = lane; c < b0; c += 64) s = fma(row[c], w[c], s);
+      for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+      if (lane == 0) part[0][i] = s;
+    }
     __syncthreads();
-    for (int i = j + 1 + tid; i < N; i += nt) w[i] -= L[(size_t)i * N + j] * wj;
-    if (tid == 0) w[j] = wj;
+    if (wv == 0) {
+      double v = ((b0 + lane == 0) ? 1.0 : 0.0) - (lane < nb ? part[0][lane] : 0.0);
+      for (int c = 0; c < nb; ++c) {
+        const double wc = __shfl(v, c, 64) / blk[c][c];
+        if (lane == c) v = wc;
+        else if (lane > c) v = fma(-blk[lane][c], wc, v);
+      }
+      if (lane < nb) w[b0 + lane] = v;
+    }
     __syncthreads();
   }
-  // backward: Lᵀ y = w  (Lᵀ[i][j] = L[j][i])
-  for (int j = N - 1; j >= 0; --j) {
-    const double yj = w[j] / L[(size_t)j * N + j];
+  // backward: Lᵀ y = w (y overwrites w), blocks from the end
+  for (int b0 = ((N - 1) / 64) * 64; b0 >= 0; b0 -= 64) {
+    const int nb = min(64, N - b0);
+    for (int idx = tid; idx < 64 * 64; idx += nt) {
+      const int i = idx >> 6, c = idx & 63;
+      blk[i][c] = (i < nb && c < nb) ? L[(size_t)(b0 + i) * N + b0 + c] : 0.0;
+    }
+    // t_c = Σ_{i >= b0+64} L[i][b0+c] y_i: thread (wv, lane = c), rows i = b0+64+wv, += 16
+    {
+      double s = 0.0;
+      if (lane < nb)
+        for (int i = b0 + 64 + wv; i < N; i += 16) s = fma(L[(size_t)i * N + b0 + lane], w[i], s);
+      part[wv][lane] = s;
+    }
     __syncthreads();
-    for (int i = tid; i < j; i += nt) w[i] -= L[(size_t)j * N + i] * yj;
-    if (tid == 0) w[j] = yj;
+    if (wv == 0) {
+      double t = 0.0;
+      for (int g = 0; g < 16; ++g) t += part[g][lane];
+      double v = lane < nb ? w[b0 + lane] - t : 0.0;
+      for (int c = nb - 1; c >= 0; --c) {
+        const double yc = __shfl(v, c, 64) / blk[c][c];
+        if (lane == c) v = yc;
+        else if (lane < c) v = fma(-blk[c][lane], yc, v);
+      }
+      if (lane < nb) w[b0 + lane] = v;
+    }
     __syncthreads();
   }
   // k_j = Σ_{i<=j} p(j-i) y_i ; kx = Σ_j k_j Px[j,:]
@@ -222,56 +345,96 @@ __global__ void zmpc_scan_matrices(double T, double T2_2, double T3_6,
   }
 }
 
-// 5a. X = L⁻¹ Puᵀ: one thread per column c, forward substitution with L broadcast across the
-// wave (every lane reads the same L element).  Puᵀ[i][c] = p(c-i) for i <= c.
-__global__ void zmpc_solve_LPuT(int N, const double* __restrict__ L, const double* __restrict__ p,
-                                double* __restrict__ X) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= N) return;
-  for (int i = 0; i < N; ++i) {
-    double s = (i <= c) ? p[c - i] : 0.0;
-    for (int j = 0; j < i; ++j) s = fma(-L[(size_t)i * N + j], X[(size_t)j * N + c], s);
-    X[(size_t)i * N + c] = s / L[(size_t)i * N + i];
+// 5a. X = L⁻¹ Puᵀ (N×N, X starts as Puᵀ: X[i][c] = p(c−i), i <= c): blocked forward
+// substitution, one launch per 16-row block r0, one wave per 16-column tile c0.  The wave forms
+// T = X[r0.., c0..] − L[r0.., :r0]·X[:r0, c0..] with v_mfma_f64_16x16x4_f64, then solves
+// Lbb·Y = T column by column (lane r owns column r; Lbb staged in LDS).
+__global__ void zmpc_init_PuT(int N, const double* __restrict__ p, double* __restrict__ X) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= N * N) return;
+  const int i = idx / N, c = idx % N;
+  X[idx] = (i <= c) ? p[c - i] : 0.0;
+}
+
+__global__ void __launch_bounds__(64) zmpc_trsm_panel(int N, int r0, const double* __restrict__ L,
+                                                      double* __restrict__ X) {
+  __shared__ double sT[16][17];
+  __shared__ double sL[16][17];
+  const int lane = threadIdx.x, r = lane & 15, kq = lane >> 4;
+  const int c0 = 16 * blockIdx.x;
+  const int ar = r0 + r, xc = c0 + r;
+  const bool aok = ar < N, cok = xc < N;
+  const double* La = L + (size_t)(aok ? ar : 0) * N;
+  dbl4 acc = {0.0, 0.0, 0.0, 0.0};
+  for (int k0 = 0; k0 < r0; k0 += 16) {
+    double a[4], b[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int kk = k0 + 4 * kq + u;
+      a[u] = aok ? La[kk] : 0.0;                         // A[i = r][k] = L[r0+r][kk]
+      b[u] = cok ? X[(size_t)kk * N + xc] : 0.0;         // B[k][j = r] = X[kk][c0+r]
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u], b[u], acc, 0, 0, 0);
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int i = kq + 4 * q;  // row of the tile, column r
+    sT[i][r] = (r0 + i < N && cok) ? X[(size_t)(r0 + i) * N + xc] - acc[q] : 0.0;
+    sL[i][r] = (r0 + i < N && r0 + r < N) ? L[(size_t)(r0 + i) * N + r0 + r]
+                                          : (i == r ? 1.0 : 0.0);
+  }
+  __syncthreads();
+  double y[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    double v = sT[i][r];
+#pragma unroll
+    for (int m = 0; m < i; ++m) v = fma(-sL[i][m], y[m], v);
+    y[i] = v / sL[i][i];
+  }
+  if (kq == 0 && cok) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (r0 + i < N) X[(size_t)(r0 + i) * N + xc] = y[i];
   }
 }
 
-// 5b. v = first column of Pu⁻¹ (lower-triangular Toeplitz again): p * v = e0, one thread.
-__global__ void zmpc_toeplitz_inverse(int N, const double* __restrict__ p,
-                                      double* __restrict__ v) {
-  if (blockIdx.x != 0 || threadIdx.x != 0) return;
-  const double p0 = p[0];
-  v[0] = 1.0 / p0;
-  for (int k = 1; k < N; ++k) {
+// 5b. v = first column of Pu⁻¹ (lower-triangular Toeplitz again): p * v = e0, i.e.
+// v_k = −(Σ_{j=1..k} p_j v_{k−j}) / p0 — sequential in k, each sum a wave reduction; p and v in
+// LDS.  One wave.
+__global__ void __launch_bounds__(64) zmpc_toeplitz_inverse(int N, const double* __restrict__ p,
+                                                            double* __restrict__ v) {
+  extern __shared__ double sm[];  // p [N], v [N]
+  double* sp = sm;
+  double* sv = sm + N;
+  const int lane = threadIdx.x;
+  for (int j = lane; j < N; j += 64) sp[j] = p[j];
+  __syncthreads();
+  const double p0 = sp[0];
+  if (lane == 0) sv[0] = 1.0 / p0;
+  __syncthreads();
+  for (int kk = 1; kk < N; ++kk) {
     double s = 0.0;
-    for (int j = 1; j <= k; ++j) s = fma(p[j], v[k - j], s);
-    v[k] = -s / p0;
+    for (int j = 1 + lane; j <= kk; j += 64) s = fma(sp[j], sv[kk - j], s);
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    if (lane == 0) sv[kk] = -s / p0;
+    __syncthreads();
   }
+  for (int j = lane; j < N; j += 64) v[j] = sv[j];
 }
 
 template <class Op>
 static void launch_gram(int N, Op op, double alpha, double diag, double* C, hipStream_t s) {
   if (N >= 64) {
     const int tiles = (N + 15) / 16;
-    hipLaunchKernelGGL(zmpc_gram_mfma<Op>, dim3(tiles * tiles), dim3(64), 0, s, N, op, alpha,
-                       diag, C);
+    const size_t lds = Op::kStaged ? sizeof(double) * N : 0;
+    hipLaunchKernelGGL(zmpc_gram_mfma<Op>, dim3(tiles * (tiles + 1) / 2), dim3(64), lds, s, N,
+                       op, alpha, diag, C);
   } else {
     hipLaunchKernelGGL(zmpc_gram_fma<Op>, dim3((N * N + 255) / 256), dim3(256), 0, s, N, op,
                        alpha, diag, C);
   }
-}
-
-static hipError_t launch_gram_pu(const zmpc_plan* P, double diag, hipStream_t s) {
-  PuOp op{P->p, P->N};
-  const int N = P->N;
-  if (N >= 64) {
-    const int tiles = (N + 15) / 16;
-    hipLaunchKernelGGL(zmpc_gram_mfma<PuOp>, dim3(tiles * tiles), dim3(64), 0, s, N, op, 1.0,
-                       diag, P->M);
-  } else {
-    hipLaunchKernelGGL(zmpc_gram_fma<PuOp>, dim3((N * N + 255) / 256), dim3(256), 0, s, N, op,
-                       1.0, diag, P->M);
-  }
-  return hipGetLastError();
 }
 
 // FFT tables (rollout.hip, long walks): twiddles e^{−2πi m/PT}, m < PT (sincospi: the
@@ -307,26 +470,47 @@ __global__ void zmpc_fft_gain(int N, const double* __restrict__ k, const double*
   g[2 * idx + 1] = im / P;
 }
 
-hipError_t zmpc_launch_plan(zmpc_plan* P, hipStream_t s) {
+hipError_t zmpc_launch_plan(zmpc_plan* P, hipStream_t s, hipEvent_t* ev) {
   const int N = P->N;
   hipError_t e;
+  // stage boundary i: ev[i] (recorded at most once, in order)
+  int stage = 0;
+  auto mark = [&](int upto) -> hipError_t {
+    if (!ev) return hipSuccess;
+    for (; stage <= upto; ++stage) {
+      hipError_t r = hipEventRecord(ev[stage], s);
+      if (r != hipSuccess) return r;
+    }
+    return hipSuccess;
+  };
+  if ((e = mark(0)) != hipSuccess) return e;
   hipLaunchKernelGGL(zmpc_build_prediction, dim3((N + 255) / 256), dim3(256), 0, s, N, P->T,
                      P->T2_2, P->T3_6, P->hg, P->Thg, P->p, P->Px);
   if ((e = hipGetLastError()) != hipSuccess) return e;
+  if ((e = mark(1)) != hipSuccess) return e;
   // M = PuᵀPu + (R/Q) I   (zmp_controller.py:198: Pu.T @ Pu + self.config.R/self.config.Q * eye)
-  if ((e = launch_gram_pu(P, P->R / P->Q, s)) != hipSuccess) return e;
-  if ((e = hipMemcpyAsync(P->L, P->M, sizeof(double) * N * N, hipMemcpyDeviceToDevice, s)) !=
-      hipSuccess)
-    return e;
-  hipLaunchKernelGGL(zmpc_cholesky, dim3(1), dim3(1024), sizeof(double) * N, s, N, P->L,
-                     P->info);
+  launch_gram(N, PuOp{P->p, N}, 1.0, P->R / P->Q, P->M, s);
   if ((e = hipGetLastError()) != hipSuccess) return e;
+  if ((e = mark(2)) != hipSuccess) return e;
+  if ((e = hipMemsetAsync(P->info, 0, sizeof(int), s)) != hipSuccess) return e;
+  for (int p0 = 0; p0 < N; p0 += 16) {
+    hipLaunchKernelGGL(zmpc_chol_panel, dim3((N - p0 + 15) / 16), dim3(64), 0, s, N, p0, P->M,
+                       P->L, P->info);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  if ((e = mark(3)) != hipSuccess) return e;
+  // w[N] (up to 32 KiB at N = 4096) on top of ≈42 KiB of static LDS
+  if ((e = hipFuncSetAttribute((const void*)zmpc_gain, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               96 * 1024)) != hipSuccess)
+    return e;
   hipLaunchKernelGGL(zmpc_gain, dim3(1), dim3(1024), sizeof(double) * N, s, N, P->Kpad, P->L,
                      P->p, P->Px, P->k, P->kx);
   if ((e = hipGetLastError()) != hipSuccess) return e;
+  if ((e = mark(4)) != hipSuccess) return e;
   hipLaunchKernelGGL(zmpc_scan_matrices, dim3(1), dim3(64), 0, s, P->T, P->T2_2, P->T3_6, P->kx,
                      P->scanP);
   if ((e = hipGetLastError()) != hipSuccess) return e;
+  if ((e = mark(5)) != hipSuccess) return e;
   if (P->fft_tw && P->fft_g) {
     hipLaunchKernelGGL(zmpc_fft_twiddles, dim3(kFftPT / 256), dim3(256), 0, s, P->fft_tw);
     if ((e = hipGetLastError()) != hipSuccess) return e;
@@ -334,25 +518,26 @@ hipError_t zmpc_launch_plan(zmpc_plan* P, hipStream_t s) {
                        P->fft_tw, P->fft_g);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
+  if ((e = mark(6)) != hipSuccess) return e;
   if (P->strict) {
-    hipLaunchKernelGGL(zmpc_solve_LPuT, dim3((N + 63) / 64), dim3(64), 0, s, N, P->L, P->p,
-                       P->X);
+    hipLaunchKernelGGL(zmpc_init_PuT, dim3((N * N + 255) / 256), dim3(256), 0, s, N, P->p, P->X);
     if ((e = hipGetLastError()) != hipSuccess) return e;
-    DenseOp op{P->X, N};
-    if (N >= 64) {
-      const int tiles = (N + 15) / 16;
-      hipLaunchKernelGGL(zmpc_gram_mfma<DenseOp>, dim3(tiles * tiles), dim3(64), 0, s, N, op,
-                         1.0 / P->Q, 0.0, P->G);
-    } else {
-      hipLaunchKernelGGL(zmpc_gram_fma<DenseOp>, dim3((N * N + 255) / 256), dim3(256), 0, s, N,
-                         op, 1.0 / P->Q, 0.0, P->G);
+    for (int r0 = 0; r0 < N; r0 += 16) {
+      hipLaunchKernelGGL(zmpc_trsm_panel, dim3((N + 15) / 16), dim3(64), 0, s, N, r0, P->L, P->X);
+      if ((e = hipGetLastError()) != hipSuccess) return e;
     }
+    if ((e = mark(7)) != hipSuccess) return e;
+    launch_gram(N, DenseOp{P->X, N}, 1.0 / P->Q, 0.0, P->G, s);
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = mark(8)) != hipSuccess) return e;
     // z-space Hessian H = Q·I + R·Pu⁻ᵀPu⁻¹ for the primal side of the strict active set
-    hipLaunchKernelGGL(zmpc_toeplitz_inverse, dim3(1), dim3(64), 0, s, N, P->p, P->v);
+    hipLaunchKernelGGL(zmpc_toeplitz_inverse, dim3(1), dim3(64), 2 * sizeof(double) * N, s, N,
+                       P->p, P->v);
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    if ((e = mark(9)) != hipSuccess) return e;
     launch_gram(N, ToeplitzOp{P->v, N}, P->R, P->Q, P->Hz, s);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
-  return hipSuccess;
+  // stage 10 (the strict LQ table) and the total are recorded by the caller
+  return mark(10);
 }

@@ -87,6 +87,8 @@ struct LqArgs {
   double rho, quu0;      // ρ, π² + ρ
   double gipi, gam2, pig;  // γ/π, γ², πγ
   double tolnu;          // multiplier tolerance in the scaled objective (1e-13 / Q)
+  int dbg;               // ZMPC_DEBUG_LQ (A/B diagnostics only): bit 0 = every wave reads the
+                         // staged bounds of group 0 (window traffic from cache; results wrong)
 };
 
 struct Ric {  // value function V(x) = ½xᵀPx − sᵀx
@@ -511,7 +513,7 @@ __global__ void __launch_bounds__(64 * G, W)
   Lane L;
   L.lane = lane;
   {
-    const int64_t g = a.shared ? 0 : (b0 >> 6);
+    const int64_t g = (a.shared || (a.dbg & 1)) ? 0 : (b0 >> 6);
     const int64_t off = ((int64_t)axis * a.groups + g) * a.rows * 64;
     L.hl = a.hl + off;
   }
@@ -832,6 +834,11 @@ void fill_consts(const zmpc_plan* p, LqArgs& a) {
   }();
   a.drift = drift;
   a.cnt = p->lqcnt;
+  static const int dbg = [] {
+    const char* e = getenv("ZMPC_DEBUG_LQ");
+    return e ? atoi(e) : 0;
+  }();
+  a.dbg = dbg;
 }
 
 hipError_t launch_lq(const zmpc_plan* p, LqArgs& a, int64_t waves, hipStream_t s) {

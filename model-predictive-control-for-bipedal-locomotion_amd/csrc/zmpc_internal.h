@@ -56,14 +56,19 @@ struct zmpc_plan {
   // gain kernel g[d] = k_{d−1} (d = 1..N), DFT(g)/P, at complex offset P − kFftPmin
   double* fft_tw = nullptr;
   double* fft_g = nullptr;
+  // plan-build stage durations (zmpc_plan_timings), milliseconds
+  float stage_ms[ZMPC_PLAN_STAGES] = {};
 };
 
 constexpr int kFftPT = 8192;    // largest transform (twiddle table size)
 constexpr int kFftPmin = 256;   // smallest transform with a gain spectrum
 constexpr int kFftGComplex = 2 * kFftPT - kFftPmin;  // Σ_P P over P = kFftPmin..kFftPT
 
-// kernels launchers (plan.hip)
-hipError_t zmpc_launch_plan(zmpc_plan* p, hipStream_t s);
+// kernels launchers (plan.hip); ev (may be NULL): ZMPC_PLAN_STAGES events, ev[0] recorded
+// before the first stage and ev[i + 1] after stage i for stages 0..9 of include/zmpc.h
+// zmpc_plan_timings (stages the plan skips record their event right after the previous one);
+// the caller records ev[11] after stage 10 (the strict LQ table)
+hipError_t zmpc_launch_plan(zmpc_plan* p, hipStream_t s, hipEvent_t* ev);
 
 // batched CoP-bound producer (cop.hip): params [B][7] = distance, step_length, foot_spread,
 // ssp, dsp, standing, dt; n_cap = 0 counts only (n_out)

@@ -12,8 +12,12 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ZMPC_LIB", os.path.join(_HERE, "libzmpc.so"))
 
-ABI_VERSION = 4  # include/zmpc.h ZMPC_ABI_VERSION this binding is written for
+ABI_VERSION = 5  # include/zmpc.h ZMPC_ABI_VERSION this binding is written for
 NCOUNTERS = 8    # include/zmpc.h ZMPC_NCOUNTERS
+PLAN_STAGES = 12  # include/zmpc.h ZMPC_PLAN_STAGES
+PLAN_STAGE_NAMES = ("prediction", "gram_PuTPu", "cholesky", "gain", "scan", "fft_tables",
+                    "strict_X", "strict_gram_G", "strict_Pu_inverse", "strict_gram_Hz",
+                    "strict_lq_table", "total")
 HERDT_MAX_FACETS = 16  # include/zmpc.h ZMPC_HERDT_MAX_FACETS
 
 ZMPC_OK = 0
@@ -25,6 +29,7 @@ ZMPC_ESTATE = -4
 ST_MAXITER = 1
 ST_NONFINITE = 2
 ST_FACTOR = 4
+ST_INFEASIBLE = 8
 
 EXPORT_P, EXPORT_PX, EXPORT_M, EXPORT_K, EXPORT_KX, EXPORT_G, EXPORT_L, EXPORT_HZ = range(8)
 
@@ -43,6 +48,8 @@ SIGNATURES = {
                                         ctypes.POINTER(ctypes.c_double), ctypes.c_int64]),
     "zmpc_plan_counters": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64),
                                           ctypes.c_int32, ctypes.c_int32]),
+    "zmpc_plan_timings": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float),
+                                         ctypes.c_int32]),
     "zmpc_step": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, _c_dbl_p, _c_dbl_p, _c_dbl_p,
                                  _c_dbl_p, ctypes.c_void_p, ctypes.c_void_p]),
     "zmpc_rollout": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, _c_dbl_p,

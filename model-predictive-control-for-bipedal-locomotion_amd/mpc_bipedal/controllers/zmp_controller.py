@@ -15,6 +15,7 @@ Additions (not in the reference): ``generate_com_trajectory_batch`` /
 disturbance scenarios at once, taking and returning torch device tensors.
 """
 
+import warnings
 from typing import Optional, Tuple
 
 import numpy as np
@@ -26,6 +27,7 @@ from ..solver import get_plan
 from . import herdt
 
 _FAILED = "QP solver did not find a solution (infeasible or other)."
+_ST_MAXITER = 1  # include/zmpc.h ZMPC_ST_MAXITER
 
 
 class ZMPController:
@@ -49,6 +51,22 @@ class ZMPController:
     def _raise_on_status(self, status):
         if int(status.max().item() if status.numel() else 0) != 0:
             raise RuntimeError(_FAILED)
+
+    def _herdt_status(self, status):
+        """Herdt drop-ins: the reference never raises on a failed joint QP — it prints a message
+        and continues (zmp_controller.py:796-802).  A walk that reached the active-set pass cap
+        (ZMPC_ST_MAXITER) therefore warns and keeps the kernel's last iterate (the reference
+        would substitute zero jerk and the air foot); any other flag (non-finite, factor,
+        infeasible polytope) raises RuntimeError."""
+        st = status.cpu().numpy() if isinstance(status, torch.Tensor) else np.asarray(status)
+        if st.size and np.any(st & ~_ST_MAXITER):
+            raise RuntimeError(_FAILED)
+        if st.size and np.any(st & _ST_MAXITER):
+            msg = (f"Joint QP solver failed: active-set pass cap reached in "
+                   f"{int(np.count_nonzero(st & _ST_MAXITER))} walk(s); continuing with the last "
+                   f"iterate")
+            print(msg)
+            warnings.warn(msg, RuntimeWarning, stacklevel=3)
 
     def _kick(self) -> float:
         # zmp_controller.py:106: dt * F_ext / m, subtracted from the y velocity
@@ -131,7 +149,8 @@ class ZMPController:
         x0 = np.stack([np.asarray(x_init, np.float64).reshape(3),
                        np.asarray(y_init, np.float64).reshape(3)])[None]
         kick = np.array([self._kick()]) if self.config.add_force else None
-        hist, foot = self._herdt_rollout(x0, v_ref, herdt.encode_states(state_ref), kick, n // 2)
+        hist, foot, _ = self._herdt_rollout(x0, v_ref, herdt.encode_states(state_ref), kick,
+                                            n // 2)
         hist, foot = hist[0].cpu().numpy(), foot[0].cpu().numpy()
         for i in np.nonzero(np.any(foot[1:] != foot[:-1], axis=1))[0]:
             # zmp_controller.py:510 (the footstep adopted when a single support ends)
@@ -156,16 +175,19 @@ class ZMPController:
                           float(np.asarray(y_fc).reshape(-1)[0])]])
         side = np.array([0 if foot_side == "left" else 1], np.int8)
         xn, step, st = plan.herdt_step(prm, x, v, win, cur, foot, side)
-        self._raise_on_status(st)
+        self._herdt_status(st)
         xn, step = xn[0].cpu().numpy(), step[0].cpu().numpy()
         fx = None if np.isnan(step[0]) else float(step[0])
         fy = None if np.isnan(step[1]) else float(step[1])
         return xn[0].reshape(3, 1), xn[1].reshape(3, 1), fx, fy
 
-    def generate_com_trajectory_herdt_batch(self, x_init, v_ref, state_ref, F_ext=None):
+    def generate_com_trajectory_herdt_batch(self, x_init, v_ref, state_ref, F_ext=None,
+                                            return_status: bool = False):
         """Many Herdt walks at once (addition): x_init [B,2,3] or None; v_ref [B,n,2] or a
         shared [n,2]; state_ref [B,n] or a shared [n] (State enums or int8 codes); F_ext [B]
-        or None.  Returns (com [B,n,2], hist [B,n,2,3], foot [B,n,2]) on the device."""
+        or None.  Returns (com [B,n,2], hist [B,n,2,3], foot [B,n,2]) on the device; with
+        return_status=True also the per-walk status [B] (ZMPC_ST_* flags) instead of raising
+        or warning on a failed walk."""
         v = torch.as_tensor(v_ref, dtype=torch.float64)
         n = int(v.shape[-2])
         st = herdt.encode_states(state_ref) if not isinstance(state_ref, torch.Tensor) \
@@ -182,10 +204,13 @@ class ZMPController:
         kick = None
         if F_ext is not None:
             kick = self.config.dt * np.asarray(F_ext, np.float64).reshape(B) / self.config.m
-        hist, foot = self._herdt_rollout(x0, v_ref, st, kick, n // 2)
+        hist, foot, status = self._herdt_rollout(x0, v_ref, st, kick, n // 2,
+                                                 check=not return_status)
+        if return_status:
+            return hist[..., 0], hist, foot, status
         return hist[..., 0], hist, foot
 
-    def _herdt_rollout(self, x0, v_ref, st, kick, kick_step):
+    def _herdt_rollout(self, x0, v_ref, st, kick, kick_step, check=True):
         plan = self._plan()
         N = plan.N
         st2 = np.atleast_2d(st)
@@ -197,8 +222,9 @@ class ZMPController:
             nb = nb[0]
         hist, foot, status = plan.herdt_rollout(prm, v_ref, st, nb, x0, kick=kick,
                                                 kick_step=kick_step)
-        self._raise_on_status(status)
-        return hist, foot
+        if check:
+            self._herdt_status(status)
+        return hist, foot, status
 
     # ------------------------------------------------------------------ batched additions
     def generate_state_trajectory_batch(self, x_init, z_max, z_min, F_ext=None,

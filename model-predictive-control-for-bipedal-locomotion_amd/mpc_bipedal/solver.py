@@ -6,7 +6,9 @@ streams only) and launch the HIP kernels on torch's current stream.
 """
 
 import ctypes
+import os
 import weakref
+from collections import OrderedDict
 
 import numpy as np
 import torch
@@ -14,7 +16,11 @@ import torch
 from . import _native
 from .models.lipm_model import plan_constants
 
-_PLAN_CACHE = {}
+# get_plan's cache: least recently used plans beyond ZMPC_PLAN_CACHE (default 8) are dropped
+# (a plan holds N² matrices and the FFT tables; a caller sweeping horizons, as
+# run_compare_runtime.py:139 does, would otherwise keep one per N)
+_PLAN_CACHE = OrderedDict()
+PLAN_CACHE_MAX = max(1, int(os.environ.get("ZMPC_PLAN_CACHE", "8")))
 
 
 def _device_index(backend: str) -> int:
@@ -57,14 +63,26 @@ class Plan:
 
     @property
     def handle(self):
+        return self._live()
+
+    def _live(self):
+        if self._h is None:
+            raise RuntimeError("plan was destroyed")
         return self._h
+
+    def destroy(self):
+        """Free the device plan now (zmpc_plan_destroy) instead of at garbage collection; the
+        object is unusable afterwards.  Idempotent."""
+        if self._h is not None:
+            self._finalizer()
+            self._h = None
 
     def export(self, what: int) -> np.ndarray:
         n = {0: self.N, 1: 3 * self.N, 2: self.N ** 2, 3: self.N, 4: 3, 5: self.N ** 2,
              6: self.N ** 2, 7: self.N ** 2}[what]
         buf = np.empty(n, dtype=np.float64)
         rc = _native.load().zmpc_plan_export(
-            self._h, what, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), n)
+            self._live(), what, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), n)
         _native.check(rc, "zmpc_plan_export")
         if what in (1,):
             return buf.reshape(self.N, 3)
@@ -77,12 +95,20 @@ class Plan:
         plan's launches since creation or the last reset; synchronises the device.  Strict
         solver: wave_passes .. launches; Herdt solver: the herdt_* keys."""
         buf = (ctypes.c_uint64 * _native.NCOUNTERS)()
-        rc = _native.load().zmpc_plan_counters(self._h, buf, _native.NCOUNTERS, int(reset))
+        rc = _native.load().zmpc_plan_counters(self._live(), buf, _native.NCOUNTERS, int(reset))
         _native.check(rc, "zmpc_plan_counters")
         return {"wave_passes": int(buf[0]), "instance_passes": int(buf[1]),
                 "working_set_slots": int(buf[2]), "launches": int(buf[3]),
                 "herdt_wave_passes": int(buf[4]), "herdt_instance_passes": int(buf[5]),
                 "herdt_footsteps": int(buf[6]), "herdt_footsteps_sq": int(buf[7])}
+
+    def timings(self) -> dict:
+        """Plan-build stage durations in ms (zmpc_plan_timings; HIP events on the creation
+        stream): name → ms, names as _native.PLAN_STAGE_NAMES."""
+        buf = (ctypes.c_float * _native.PLAN_STAGES)()
+        rc = _native.load().zmpc_plan_timings(self._live(), buf, _native.PLAN_STAGES)
+        _native.check(rc, "zmpc_plan_timings")
+        return {name: float(buf[i]) for i, name in enumerate(_native.PLAN_STAGE_NAMES)}
 
     # -- launches --------------------------------------------------------------------------
     def _dev(self):
@@ -107,7 +133,7 @@ class Plan:
                                                            device=self._dev())
         with torch.cuda.device(self.device):
             stream = torch.cuda.current_stream(self.device).cuda_stream
-            rc = _native.load().zmpc_step(self._h, B, _ptr(x), _ptr(zmax_win), _ptr(zmin_win),
+            rc = _native.load().zmpc_step(self._live(), B, _ptr(x), _ptr(zmax_win), _ptr(zmin_win),
                                           _ptr(out), _ptr(st), ctypes.c_void_p(stream))
         _native.check(rc, "zmpc_step")
         return out, st
@@ -171,13 +197,13 @@ class Plan:
         if status is None:
             status = torch.empty(B, dtype=torch.int32, device=self._dev())
         if isinstance(kick_step, (int, np.integer)):
-            args = (self._h, B, n, _ptr(zmax), _ptr(zmin), bstride, _ptr(x0), _ptr(kick_t),
+            args = (self._live(), B, n, _ptr(zmax), _ptr(zmin), bstride, _ptr(x0), _ptr(kick_t),
                     int(kick_step), _ptr(hist), _ptr(status))
             return hist, status, ("zmpc_rollout", args, (zmax, zmin, x0, kick_t))
         ks = torch.as_tensor(kick_step, dtype=torch.int64, device=self._dev()).contiguous()
         if tuple(ks.shape) != (B,):
             raise ValueError(f"per-walk kick_step must be [B], got {tuple(ks.shape)}")
-        args = (self._h, B, n, _ptr(zmax), _ptr(zmin), bstride, _ptr(x0), _ptr(kick_t),
+        args = (self._live(), B, n, _ptr(zmax), _ptr(zmin), bstride, _ptr(x0), _ptr(kick_t),
                 _ptr(ks), _ptr(hist), _ptr(status))
         return hist, status, ("zmpc_rollout_kicks", args, (zmax, zmin, x0, kick_t, ks))
 
@@ -195,10 +221,12 @@ class Plan:
             raise ValueError(f"x0 must be [B, 2, 3], got {tuple(x0.shape)}")
         B = int(x0.shape[0])
         v = self._as_dev(v_ref)
+        if v.dim() not in (2, 3) or v.shape[-1] != 2:
+            raise ValueError(f"v_ref must be [B, n, 2] or [n, 2], got {tuple(v.shape)}")
         n = int(v.shape[-2])
         if v.dim() == 2:
             vs = 0
-        elif v.dim() == 3 and v.shape[0] == B:
+        elif v.shape[0] == B:
             vs = 2 * n
         else:
             raise ValueError(f"v_ref must be [B, n, 2] or [n, 2], got {tuple(v.shape)}")
@@ -207,10 +235,14 @@ class Plan:
             states, torch.Tensor) else states, dtype=torch.int8, device=dev).contiguous()
         nb = torch.as_tensor(np.asarray(nb_next, dtype=np.int32) if not isinstance(
             nb_next, torch.Tensor) else nb_next, dtype=torch.int32, device=dev).contiguous()
+        # per-walk [B, n] or shared [n]: a 2-D array must carry one row per walk (the kernel
+        # reads row b of walk b)
+        for name, t in (("states", st), ("nb_next", nb)):
+            if t.dim() not in (1, 2) or t.shape[-1] != n or (t.dim() == 2 and t.shape[0] != B):
+                raise ValueError(f"{name} must be [B, n] = [{B}, {n}] or [n], got "
+                                 f"{tuple(t.shape)}")
         ss = 0 if st.dim() == 1 else n
         ns = 0 if nb.dim() == 1 else n
-        if st.shape[-1] != n or nb.shape[-1] != n:
-            raise ValueError("states and nb_next must hold n samples per walk")
         kick_t = None if kick is None else self._as_dev(kick, (B,))
         hist = torch.empty((B, n, 2, 3), dtype=torch.float64, device=dev)
         foot = torch.empty((B, n, 2), dtype=torch.float64, device=dev)
@@ -218,7 +250,7 @@ class Plan:
         with torch.cuda.device(self.device):
             stream = torch.cuda.current_stream(self.device).cuda_stream
             rc = _native.load().zmpc_herdt_rollout(
-                self._h, ctypes.byref(params), B, n, _ptr(v), vs, _ptr(st), ss, _ptr(nb), ns,
+                self._live(), ctypes.byref(params), B, n, _ptr(v), vs, _ptr(st), ss, _ptr(nb), ns,
                 _ptr(x0), _ptr(kick_t), int(kick_step), _ptr(hist), _ptr(foot), _ptr(status),
                 ctypes.c_void_p(stream))
         _native.check(rc, "zmpc_herdt_rollout")
@@ -242,7 +274,7 @@ class Plan:
         with torch.cuda.device(self.device):
             stream = torch.cuda.current_stream(self.device).cuda_stream
             rc = _native.load().zmpc_herdt_step(
-                self._h, ctypes.byref(params), B, _ptr(x), _ptr(v), _ptr(sw), _ptr(cu), _ptr(f),
+                self._live(), ctypes.byref(params), B, _ptr(x), _ptr(v), _ptr(sw), _ptr(cu), _ptr(f),
                 _ptr(sd), _ptr(xn), _ptr(step), _ptr(status), ctypes.c_void_p(stream))
         _native.check(rc, "zmpc_herdt_step")
         return xn, step, status
@@ -254,7 +286,23 @@ def get_plan(config, device=None) -> Plan:
     key = (dev, int(config.horizon), float(config.dt), float(config.h), float(config.g),
            float(config.Q), float(config.R), bool(config.strict))
     p = _PLAN_CACHE.get(key)
-    if p is None:
-        p = Plan(dev, key[1], key[2], key[3], key[4], key[5], key[6], key[7])
-        _PLAN_CACHE[key] = p
+    if p is not None and p._h is not None:
+        _PLAN_CACHE.move_to_end(key)
+        return p
+    p = Plan(dev, key[1], key[2], key[3], key[4], key[5], key[6], key[7])
+    _PLAN_CACHE[key] = p
+    while len(_PLAN_CACHE) > PLAN_CACHE_MAX:
+        # drop the cache's reference only: a caller still holding the plan keeps it alive,
+        # the device memory is freed when the last reference goes (weakref finalizer)
+        _PLAN_CACHE.popitem(last=False)
     return p
+
+
+def clear_plan_cache(destroy: bool = False):
+    """Empty get_plan's cache; with destroy=True also free every cached plan now (callers must
+    not use those plans afterwards)."""
+    plans = list(_PLAN_CACHE.values())
+    _PLAN_CACHE.clear()
+    if destroy:
+        for p in plans:
+            p.destroy()

@@ -1,0 +1,31 @@
+#!/usr/bin/env python3
+"""Plan-build stage timings (zmpc_plan_timings) over horizons, one JSON line per plan.
+Usage (GPU box): python scripts/plan_timing.py [N ...]"""
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "model-predictive-control-for-bipedal-locomotion_amd"))
+import torch  # noqa: E402
+from mpc_bipedal.solver import Plan  # noqa: E402
+
+Ns = [int(a) for a in sys.argv[1:]] or [64, 150, 300, 512, 1024, 2048, 4096]
+torch.cuda.init()
+Plan(0, 150, 0.01, 0.75, 9.81, 1.0, 1e-6, True)  # warm the module / first-launch costs
+for N in Ns:
+    for strict in (False, True):
+        if strict and N > 2560:
+            continue
+        t0 = time.perf_counter()
+        p = Plan(0, N, 1.5 / N, 0.75, 9.81, 1.0, 1e-6, strict)
+        wall = (time.perf_counter() - t0) * 1e3
+        t = p.timings()
+        gram_flop = 2.0 * N ** 3 / 3.0  # PuᵀPu of a lower-triangular Toeplitz Pu (structure)
+        line = {"N": N, "strict": strict, "wall_ms": wall,
+                "stages_ms": {k: round(v, 4) for k, v in t.items() if v > 0},
+                "gram_tflops": gram_flop / (t["gram_PuTPu"] * 1e-3) / 1e12
+                if t["gram_PuTPu"] > 0 else None}
+        print(json.dumps(line), flush=True)
+        p.destroy()

@@ -68,3 +68,49 @@ def test_gloo_two_ranks_reassemble(tmp_path, total):
     mp.start_processes(_worker, args=(2, _free_port(), total, out), nprocs=2, join=True,
                        start_method="spawn")
     assert float(np.load(out)) == 0.0
+
+
+def test_bench_launcher_two_ranks_stub():
+    """`python bench.py --gpus 2` (no torchrun around it) starts two ranks itself: spawn →
+    shard → timed region → all-gather → ONE JSON line from rank 0 with n_gpus 2 (gloo, stub
+    per-rank solver; the GPU form runs the same code with RCCL)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
+                        "--stub-solver", "--steps", "3", "--warmup", "1", "--batch", "5"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["world_size"] == 2
+    assert line["config"]["global_batch"] == 10 and line["config"]["parallelism"] == "dp2"
+    assert line["gather_ok"] is True and line["allgather_ms"] is not None
+    assert line["steps"] == 3 and line["value"] > 0
+
+
+def test_bench_rejects_world_size_mismatch():
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
+                        "--stub-solver"], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and "WORLD_SIZE" in r.stderr
+
+
+def test_bench_harness_cpu_leg_semantics():
+    """bench.harness_cpu_seconds follows run_compare_runtime.py:36-73 (3 warm-ups, mean of 10
+    `_run_once` = 2 solves) on the CPU port, both branches."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    if root not in sys.path:
+        sys.path.insert(0, root)
+    import bench
+    for strict in (False, True):
+        t = bench.harness_cpu_seconds(10, strict)
+        assert 0.0 < t < 1.0

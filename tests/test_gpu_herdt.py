@@ -121,3 +121,77 @@ def test_herdt_work_counters():
     assert k["herdt_instance_passes"] >= 2 * B * (n - 1)
     assert k["herdt_wave_passes"] * 64 >= k["herdt_instance_passes"]
     assert k["herdt_footsteps_sq"] >= k["herdt_footsteps"] >= 0
+
+
+def _ragged_schedules(B, n=90):
+    """B walks of n samples cut from the default schedule at staggered offsets (the footstep
+    count m of the windows differs between the walks of one 32-walk wave), each with its own
+    forward speed."""
+    d = golden("herdt_default.npz")
+    states = np.stack([d["states"][40 + 3 * b: 40 + 3 * b + n] for b in range(B)])
+    v = np.zeros((B, n, 2))
+    v[:, :, 0] = np.where(states == 0, 0.0, (0.12 + 0.004 * np.arange(B))[:, None])
+    return states, v
+
+
+def test_herdt_per_walk_schedules_equal_single_walks():
+    """Per-walk [B,n] states and [B,n,2] v_ref with B = 37 (not a multiple of the 32 walks of a
+    wave: invalid-lane clamping), footstep counts differing inside a wave (zero-padded footstep
+    columns): every walk equals the same walk launched alone (whose path is pinned to the
+    reference-driven golden and to the oracle by the tests above)."""
+    B = 37
+    states, v = _ragged_schedules(B)
+    cfg = MPCConfig(method="herdt", add_force=True, F_ext=300.0)
+    c = ZMPController(cfg)
+    rng = np.random.default_rng(9)
+    x0 = np.zeros((B, 2, 3))
+    x0[:, :, 0] = rng.uniform(-0.01, 0.01, (B, 2))
+    F = rng.uniform(0.0, 600.0, B)
+    com, hist, foot = c.generate_com_trajectory_herdt_batch(x0, v, states, F_ext=F)
+    com, foot = com.cpu().numpy(), foot.cpu().numpy()
+    n = states.shape[1]
+    # the windows really differ in footstep count inside the first wave
+    pad = np.concatenate([states, np.repeat(states[:, -1:], cfg.horizon, axis=1)], axis=1)
+    ms = {H.max_footsteps(pad[b:b + 1], cfg.horizon, n) for b in range(32)}
+    assert len(ms) > 1
+    for b in range(B):
+        cb, _, fb = c.generate_com_trajectory_herdt_batch(x0[b:b + 1], v[b], states[b],
+                                                          F_ext=F[b:b + 1])
+        assert rmse(com[b], cb[0].cpu().numpy()) <= 1e-9, b
+        assert np.abs(foot[b] - fb[0].cpu().numpy()).max() <= 1e-9, b
+
+
+def test_herdt_rollout_rejects_mismatched_batches():
+    """states / nb_next / v_ref given per walk must carry one row per walk."""
+    d = golden("herdt_default.npz")
+    c = ZMPController(MPCConfig(method="herdt"))
+    plan = c._plan()
+    n = len(d["states"])
+    prm = H.make_params(c.config, 7)
+    x0 = np.zeros((3, 2, 3))
+    nb = np.zeros(n, np.int32)
+    with pytest.raises(ValueError, match="states"):
+        plan.herdt_rollout(prm, d["v_ref"], np.stack([d["states"]] * 2), nb, x0)
+    with pytest.raises(ValueError, match="nb_next"):
+        plan.herdt_rollout(prm, d["v_ref"], d["states"], np.zeros((1, n), np.int32), x0)
+    with pytest.raises(ValueError, match="v_ref"):
+        plan.herdt_rollout(prm, np.stack([d["v_ref"]] * 2), d["states"], nb, x0)
+    with pytest.raises(ValueError, match="v_ref"):
+        plan.herdt_rollout(prm, np.zeros((n, 3)), d["states"], nb, x0)
+
+
+def test_herdt_too_many_footsteps_flags_the_wave():
+    """A batch whose windows hold more footsteps than params.max_footsteps: every walk of the
+    affected wave reports a non-zero status — including a standing walk (no footsteps) that
+    shares the wave (no walk reports success from a truncated solve)."""
+    d = golden("herdt_default.npz")
+    c = ZMPController(MPCConfig(method="herdt"))
+    plan = c._plan()
+    n = len(d["states"])
+    states = np.stack([d["states"]] * 3 + [np.zeros(n, np.int8)])
+    pad = np.concatenate([states, np.repeat(states[:, -1:], plan.N, axis=1)], axis=1)
+    nb = np.array([[t[0] for t in H.find_nb_steps(p)][:n] for p in pad], np.int32)
+    assert H.max_footsteps(pad[:1], plan.N, n) >= 3 and H.max_footsteps(pad[3:], plan.N, n) == 0
+    prm = H.make_params(c.config, 2)  # too small on purpose
+    _, _, st = plan.herdt_rollout(prm, d["v_ref"], states, nb, np.zeros((4, 2, 3)))
+    assert np.all(st.cpu().numpy() != 0)

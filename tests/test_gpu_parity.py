@@ -765,3 +765,45 @@ def test_fft_correlation_equals_direct(N, n, tmp_path):
     assert np.abs(h["1"] - h["0"]).max() <= 1e-11
     h_auto = h_auto.cpu().numpy()
     assert np.array_equal(h_auto, h["1"]) or np.array_equal(h_auto, h["0"])
+
+
+# ------------------------------------------------ plan build at long horizons
+
+
+@pytest.mark.parametrize("N,strict", ((1000, False), (700, True), (2048, False)))
+def test_plan_blocked_factorisation_long_horizon(N, strict):
+    """The blocked Cholesky (16-column MFMA panels), the blocked gain solves and (strict) the
+    blocked L⁻¹Puᵀ at horizons past a single panel row: L·Lᵀ = M, the gain row equals the
+    oracle's dense solve, G = inv(Hz)."""
+    dt = 1.5 / N
+    p = plan(N, strict=strict)
+    Px, Pu = O.prediction_matrices(N, dt, H, G)
+    Mref = Pu.T @ Pu + R / Q * np.eye(N)
+    M = p.export(_native.EXPORT_M)
+    assert np.abs(M - Mref).max() <= 1e-13 * np.abs(Mref).max()
+    Lf = p.export(_native.EXPORT_L)
+    assert np.array_equal(np.triu(Lf, 1), np.zeros_like(Lf))
+    assert np.abs(Lf @ Lf.T - Mref).max() <= 1e-12 * np.abs(Mref).max()
+    k, kx = O.gain_row(N, dt, H, G, Q, R)
+    assert np.abs(p.export(_native.EXPORT_K) - k).max() <= 1e-8 * np.abs(k).max()
+    assert np.allclose(p.export(_native.EXPORT_KX), kx, rtol=1e-8, atol=0)
+    t = p.timings()
+    assert t["total"] > 0 and t["cholesky"] > 0 and t["gram_PuTPu"] > 0
+    if strict:
+        Hz, V, _, _ = O.strict_matrices(N, dt, H, G, Q, R)
+        Gref = np.linalg.inv(Hz)
+        assert np.abs(p.export(_native.EXPORT_G) - Gref).max() <= 1e-9 * np.abs(Gref).max()
+        assert np.abs(p.export(_native.EXPORT_HZ) - Hz).max() <= 1e-9 * np.abs(Hz).max()
+
+
+def test_plan_cache_bounded_and_destroy():
+    from mpc_bipedal import solver
+    solver.clear_plan_cache(destroy=True)
+    for N in range(10, 10 + 10 * (solver.PLAN_CACHE_MAX + 3), 10):
+        get_plan(MPCConfig(horizon=N))
+    assert len(solver._PLAN_CACHE) == solver.PLAN_CACHE_MAX
+    p = plan(32)
+    p.destroy()
+    p.destroy()  # idempotent
+    with pytest.raises(RuntimeError, match="destroyed"):
+        p.export(_native.EXPORT_K)

@@ -92,7 +92,7 @@ def test_library_loads_and_exports_every_symbol():
     exported = set(re.findall(r" T (zmpc_\w+)", out))
     assert set(_header_symbols()) <= exported
     lib = _native.load()
-    assert lib.zmpc_abi_version() == _native.ABI_VERSION == 4
+    assert lib.zmpc_abi_version() == _native.ABI_VERSION == 5
     assert lib.zmpc_last_error() == b""
 
 
@@ -124,6 +124,9 @@ def test_argument_errors_without_gpu():
     rc = lib.zmpc_herdt_step(None, None, 1, None, None, None, None, None, None, None, None,
                              None, None)
     assert rc == _native.ZMPC_EINVAL
+    tbuf = (ctypes.c_float * _native.PLAN_STAGES)()
+    rc = lib.zmpc_plan_timings(None, tbuf, _native.PLAN_STAGES)
+    assert rc == _native.ZMPC_EINVAL and b"NULL" in lib.zmpc_last_error()
 
 
 def test_router_errors():
