@@ -236,6 +236,27 @@ def _herdt_cpu_baseline(cfg, v_ref, st, hist_gpu, foot_gpu, x0_h, kick_h, budget
             "seconds": el, "max_abs_state_gpu_vs_port": err}
 
 
+def plan_record(plan):
+    """The batch-invariant plan build (charged once per plan, never per solve):
+    zmpc_plan_timings stage durations (HIP events on the creation stream) and the FP64 MFMA
+    Gram M = PuᵀPu + (R/Q)·I (zmp_controller.py:198): its algorithmic FLOPs — 2N³/3 for the
+    product of a lower-triangular Toeplitz Pu with itself (Σ_ab 2(N − max(a, b))); the
+    reference's dense Pu.T @ Pu is 2N³ — over its event time, as a fraction of the FP64 dense
+    peak.  The rocprofv3 kernel time and MFMA counters of the same kernel are in
+    profiles/r3_plan_*."""
+    t = plan.timings()
+    N = plan.N
+    flops = 2.0 * N ** 3 / 3.0
+    g_ms = t["gram_PuTPu"]
+    tf = flops / (g_ms * 1e-3) / 1e12 if g_ms > 0 else None
+    return {"N": N, "strict": plan.strict, "build_ms": t["total"],
+            "stages_ms": {k: v for k, v in t.items() if v > 0 and k != "total"},
+            "gram": {"kernel": "zmpc_gram_mfma<ToeplitzOp>", "engine": "v_mfma_f64_16x16x4_f64",
+                     "ms": g_ms, "alg_flops": flops, "dense_equiv_flops": 2.0 * N ** 3,
+                     "tflops": tf, "frac_fp64_peak": tf / FP64_PEAK_TFS if tf else None},
+            "cholesky_ms": t["cholesky"]}
+
+
 def make_batch(B, rank, cfg, shared):
     """Bounds ([B,n,2] per walk, or the shared [n,2] CoP), x0 [B,2,3], F [B]."""
     zmax, zmin, _ = CoPGenerator(cfg).generate_cop_trajectory()
@@ -735,6 +756,7 @@ def main():
     n = zmax_h.shape[-2]
     kick_h = cfg.dt * F_h / cfg.m
     plan = Plan(dev.index, cfg.horizon, cfg.dt, cfg.h, cfg.g, cfg.Q, cfg.R, cfg.strict)
+    plan_rec = plan_record(plan)
     zmax = torch.as_tensor(zmax_h, device=dev)
     zmin = torch.as_tensor(zmin_h, device=dev)
     x0 = torch.as_tensor(x0_h, device=dev)
@@ -901,6 +923,7 @@ def main():
             "allgather_ms": gather_ms,
             "pcie_inclusive": pcie,
             "pipelined": pipelined,
+            "plan": plan_rec,
         }
         print(json.dumps(line))
     if world > 1:

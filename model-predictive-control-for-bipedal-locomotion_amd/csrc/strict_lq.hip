@@ -778,6 +778,7 @@ const LqVariant kLqVariants[] = {
     ZMPC_LQV(8, 2, 1),  // N up to 2560
     ZMPC_LQV(6, 2, 8),
     ZMPC_LQV(8, 1, 8),
+    ZMPC_LQV(4, 3, 4),  // A/B: 3 waves per SIMD (≤ 168 VGPRs), 4-wave workgroups
 };
 #undef ZMPC_LQV
 constexpr size_t kLdsCap = 160 * 1024;
