@@ -239,14 +239,17 @@ def _herdt_cpu_baseline(cfg, v_ref, st, hist_gpu, foot_gpu, x0_h, kick_h, budget
 def plan_record(plan):
     """The batch-invariant plan build (charged once per plan, never per solve):
     zmpc_plan_timings stage durations (HIP events on the creation stream) and the FP64 MFMA
-    Gram M = PuᵀPu + (R/Q)·I (zmp_controller.py:198): its algorithmic FLOPs — 2N³/3 for the
-    product of a lower-triangular Toeplitz Pu with itself (Σ_ab 2(N − max(a, b))); the
-    reference's dense Pu.T @ Pu is 2N³ — over its event time, as a fraction of the FP64 dense
-    peak.  The rocprofv3 kernel time and MFMA counters of the same kernel are in
-    profiles/r3_plan_*."""
-    t = plan.timings()
+    Gram M = PuᵀPu + (R/Q)·I (zmp_controller.py:198): its algorithmic FLOPs — the lower
+    triangle of the symmetric product of a lower-triangular Toeplitz Pu with itself,
+    Σ_{a≥b} 2(N − a) = N(N+1)(N+2)/3 (the upper half is a copy; the reference's dense
+    Pu.T @ Pu is 2N³) — over its event time, as a fraction of the FP64 dense peak.  The rocprofv3 kernel time and MFMA counters of the same kernel are in
+    profiles/r3_plan_*.  The timings are those of a second build of the same plan: the
+    first kernel launches of a process also load the code object (≈0.5 ms on the first)."""
+    again = Plan(plan.device, plan.N, plan.dt, plan.h, plan.g, plan.Q, plan.R, plan.strict)
+    t = again.timings()
+    again.destroy()
     N = plan.N
-    flops = 2.0 * N ** 3 / 3.0
+    flops = N * (N + 1) * (N + 2) / 3.0
     g_ms = t["gram_PuTPu"]
     tf = flops / (g_ms * 1e-3) / 1e12 if g_ms > 0 else None
     return {"N": N, "strict": plan.strict, "build_ms": t["total"],

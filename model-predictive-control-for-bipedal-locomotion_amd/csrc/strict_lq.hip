@@ -41,6 +41,7 @@
 // The x axis of a walk is free almost everywhere; the y axis keeps active slots through most
 // of the horizon while the robot steps (scripts/strict_active_stats.py).
 #include <cstdio>
+#include <cstring>
 #include <cstdlib>
 
 #include "zmpc_internal.h"
@@ -231,22 +232,90 @@ struct Lane {
   int lane;
 };
 
+// Per-lane working-set flags of the wave's N slots in LDS (0 free, 1 at z_max, 2 at z_min):
+// one byte per slot ([slot][64]), or, in the prefetching kernel (PK), two slots per byte
+// ([slot/2][64], low nibble = even slot) so that the segment buffers fit beside them.
+template <bool PK>
+struct Flags {
+  unsigned char* p;
+  __device__ __forceinline__ int get(int k, int lane) const {
+    if constexpr (PK)
+      return (p[(k >> 1) * 64 + lane] >> ((k & 1) << 2)) & 0xF;
+    else
+      return p[k * 64 + lane];
+  }
+  __device__ __forceinline__ void set(int k, int lane, int v) const {
+    if constexpr (PK) {
+      unsigned char* b = p + (k >> 1) * 64 + lane;
+      const int sh = (k & 1) << 2;
+      *b = (unsigned char)((*b & ~(0xF << sh)) | (v << sh));
+    } else {
+      p[k * 64 + lane] = (unsigned char)v;
+    }
+  }
+};
+
+// Segment prefetch through LDS (PK): the next segment's staged bound rows (S × 1 KiB) and
+// checkpoint (9 × 512 B, copied as five 1-KiB pieces) go global → LDS with LDS-DMA
+// (global_load_lds_dwordx4: lane-linear, no VGPR destination) while the current segment
+// computes; at 256 VGPRs (two waves per SIMD) nothing else hides the load latency, and a
+// register prefetch spills.
+template <int S>
+__device__ __forceinline__ void glds_rows(const LqArgs& a, int j, const Lane& L, int64_t i,
+                                          double2* rbuf) {
+  const int64_t row0 = i + a.toff + (int64_t)j * S;
+  const double2* hp = L.hl + row0 * 64 + L.lane;
+#pragma unroll
+  for (int q = 0; q < S; ++q)
+    __builtin_amdgcn_global_load_lds((const void*)(hp + q * 64), (void*)(rbuf + q * 64), 16, 0,
+                                     0);
+}
+
+// Pieces [c0, c1) of segment j's checkpoint in the paired layout (ck_store<PK>): piece c is the
+// [64] (double2) array of component pairs c — (p00, p01), (p02, p11), (p12, p22), (s0, s1),
+// (s2, –) — so each lane copies only its own 16 bytes (lanes outside the pass, masked off, then
+// miss nothing another lane needs).
+__device__ __forceinline__ void glds_ck(const double* ck, int j, int lane, double2* cbuf,
+                                        int c0, int c1) {
+  const double2* src = reinterpret_cast<const double2*>(ck + (size_t)j * 10 * 64) + lane;
+  for (int c = c0; c < c1; ++c)
+    __builtin_amdgcn_global_load_lds((const void*)(src + c * 64), (void*)(cbuf + c * 64), 16, 0,
+                                     0);
+}
+
+// s_waitcnt vmcnt(0) / lgkmcnt(0) (gfx9 encoding: vmcnt [3:0]+[15:14], expcnt [6:4],
+// lgkmcnt [11:8])
+__device__ __forceinline__ void wait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+__device__ __forceinline__ void wait_lgkm0() { __builtin_amdgcn_s_waitcnt(0xC07F); }
+
 // Issue the loads of segment j's slots (bounds, and the flags when FLAGS).  Slots past N read
 // padded rows (loaded, never used) so the loads carry no guards.
-template <int S, bool FLAGS>
+template <int S, bool FLAGS, class FL>
 __device__ __forceinline__ void seg_load(const LqArgs& a, int j, const Lane& L, int64_t i,
-                                         const unsigned char* fl, SegIn<S>& in) {
+                                         const FL& fl, SegIn<S>& in) {
   // segment's first row (the lane's own timestep); its S rows are 1 KiB apart: one address,
   // immediate offsets
   const int64_t row0 = i + a.toff + (int64_t)j * S;
   const double2* hp = L.hl + row0 * 64;
-  const unsigned char* fp = fl + j * S * 64;
 #pragma unroll
   for (int q = 0; q < S; ++q) {
     const double2 v = hp[q * 64 + L.lane];
     in.hi[q] = v.x;
     in.lo[q] = v.y;
-    if (FLAGS) in.f[q] = fp[q * 64 + L.lane];
+    if (FLAGS) in.f[q] = fl.get(j * S + q, L.lane);
+  }
+}
+
+// The same from the segment prefetched into LDS (rbuf: [S][64] pairs).
+template <int S, bool FLAGS, class FL>
+__device__ __forceinline__ void seg_load_lds(int j, const Lane& L, const double2* rbuf,
+                                             const FL& fl, SegIn<S>& in) {
+#pragma unroll
+  for (int q = 0; q < S; ++q) {
+    const double2 v = rbuf[q * 64 + L.lane];
+    in.hi[q] = v.x;
+    in.lo[q] = v.y;
+    if (FLAGS) in.f[q] = fl.get(j * S + q, L.lane);
   }
 }
 
@@ -335,11 +404,11 @@ __device__ __forceinline__ void seg_forward(const LqArgs& a, int j, const SegIn<
 
 // Forward through a free-tail segment (table K, kff from seg_tail): primal check and the new
 // flags (every slot here is free for every lane taking part, so no costate is needed).
-template <int S, bool FULL>
+template <int S, bool FULL, class FL>
 __device__ __forceinline__ void seg_forward_tail(const LqArgs& a, const double* __restrict__ tab,
                                                  int j, const SegIn<S>& in, const SegOut<S>& g,
                                                  double* x, double& u0, bool& changed, int& kl,
-                                                 unsigned char* fl, int lane) {
+                                                 const FL& fl, int lane) {
   const double tol = 1e-13;
 #pragma unroll
   for (int q = 0; q < S; ++q) {
@@ -356,7 +425,7 @@ __device__ __forceinline__ void seg_forward_tail(const LqArgs& a, const double* 
       x[1] = y1;
       x[2] = y2;
       const int nf = (z > in.hi[q] + tol) ? 1 : ((z < in.lo[q] - tol) ? 2 : 0);
-      fl[k * 64 + lane] = (unsigned char)nf;
+      fl.set(k, lane, nf);
       changed |= nf != 0;
       kl = nf ? k : kl;
     }
@@ -366,10 +435,10 @@ __device__ __forceinline__ void seg_forward_tail(const LqArgs& a, const double* 
 // Costate sweep back through segment j from λ at its end (λ_k = ∇V_k(x_k) = c1 e_k + Aᵀλ_{k+1},
 // e_k = Q (z_k − r_k) + ν_k): the bound multipliers ν_k of the active slots, dual check, the
 // slot's new flag; kl = the last slot active in the new set.
-template <int S, bool FULL>
+template <int S, bool FULL, class FL>
 __device__ __forceinline__ void seg_costate(const LqArgs& a, int j, const SegIn<S>& in,
                                             const SegOut<S>& g, double* lam, bool& changed,
-                                            int& kl, unsigned char* fl, int lane) {
+                                            int& kl, const FL& fl, int lane) {
 #pragma unroll
   for (int q = S - 1; q >= 0; --q) {
     const int k = j * S + q;
@@ -386,7 +455,7 @@ __device__ __forceinline__ void seg_costate(const LqArgs& a, int j, const SegIn<
         const bool rel = (f == 1 && nu < -a.tolnu) || (f == 2 && nu > a.tolnu);
         // the slot's new flag, written unconditionally (branch-free)
         const int nf = (f == 0) ? g.nf[q] : (rel ? 0 : f);
-        fl[k * 64 + lane] = (unsigned char)nf;
+        fl.set(k, lane, nf);
         changed |= nf != f;
         kl = (nf != 0 && k > kl) ? k : kl;
       }
@@ -399,10 +468,10 @@ __device__ __forceinline__ void seg_costate(const LqArgs& a, int j, const SegIn<
 }
 
 // Sweep B through one working-set segment: Riccati from its checkpoint, forward, costate.
-template <int S, bool FULL>
+template <int S, bool FULL, class FL>
 __device__ __forceinline__ void seg_sweep_b(const LqArgs& a, int j, Ric& v, const SegIn<S>& in,
                                             SegOut<S>& g, double* xs, double& u0, bool& changed,
-                                            int& kl, unsigned char* fl, int lane) {
+                                            int& kl, const FL& fl, int lane) {
   const Ric ve = v;  // V at the segment's end
   seg_riccati<S, FULL, true, false>(a, j, v, in, g);
   seg_forward<S, FULL>(a, j, in, g, xs, u0);
@@ -431,12 +500,33 @@ struct CkIO {
     else
       return *p;
   }
+  __device__ __forceinline__ void st2(double2* p, double x, double y) const {
+    typedef double v2d __attribute__((ext_vector_type(2)));
+    const v2d t = {x, y};
+    if constexpr (NT)
+      __builtin_nontemporal_store(t, reinterpret_cast<v2d*>(p));
+    else
+      *reinterpret_cast<v2d*>(p) = t;
+  }
 };
 
-template <bool NT>
+// Doubles of one segment's checkpoint per 64 lanes: [9][64], or paired [5][64] double2 (PK).
+template <bool PK>
+constexpr int ck_stride() { return PK ? 10 * 64 : 9 * 64; }
+
+template <bool PK, bool NT>
 __device__ __forceinline__ void ck_store(const CkIO<NT>& io, double* ck, int j, const Ric& v,
                                          int lane) {
-  double* p = ck + (size_t)j * 9 * 64 + lane;
+  if constexpr (PK) {
+    double2* p = reinterpret_cast<double2*>(ck + (size_t)j * ck_stride<PK>()) + lane;
+    io.st2(p + 0, v.p00, v.p01);
+    io.st2(p + 64, v.p02, v.p11);
+    io.st2(p + 128, v.p12, v.p22);
+    io.st2(p + 192, v.s0, v.s1);
+    io.st2(p + 256, v.s2, 0.0);
+    return;
+  }
+  double* p = ck + (size_t)j * ck_stride<PK>() + lane;
   io.st(p + 0, v.p00);
   io.st(p + 64, v.p01);
   io.st(p + 128, v.p02);
@@ -448,10 +538,16 @@ __device__ __forceinline__ void ck_store(const CkIO<NT>& io, double* ck, int j, 
   io.st(p + 512, v.s2);
 }
 
-template <bool NT>
+template <bool PK, bool NT>
 __device__ __forceinline__ void ck_store_s(const CkIO<NT>& io, double* ck, int j, const Ric& v,
                                            int lane) {
-  double* p = ck + (size_t)j * 9 * 64 + lane;
+  if constexpr (PK) {
+    double2* p = reinterpret_cast<double2*>(ck + (size_t)j * ck_stride<PK>()) + lane;
+    io.st2(p + 192, v.s0, v.s1);
+    io.st2(p + 256, v.s2, 0.0);
+    return;
+  }
+  double* p = ck + (size_t)j * ck_stride<PK>() + lane;
   io.st(p + 384, v.s0);
   io.st(p + 448, v.s1);
   io.st(p + 512, v.s2);
@@ -485,16 +581,26 @@ __device__ __forceinline__ void ck_load_s(const CkIO<NT>& io, const double* ck, 
 // four 64-walk groups, so each SIMD (waves w and w + 4 under the round-robin placement) holds
 // one wave of each axis — the y axis carries nearly all of the active-set work, and an
 // axis-pure SIMD would idle once its x waves are done.  G = 4 (A/B): axis = wave parity.
-template <int S, int W, int G, bool NT = false>
+// PK: segments prefetched through LDS (glds_rows / glds_ck), flags nibble-packed.
+template <int S, int W, int G, bool NT = false, bool PK = false>
 __global__ void __launch_bounds__(64 * G, W)
     zmpc_strict_lq_kernel(LqArgs a, const double* __restrict__ tab) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lq_smem[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int64_t gw = (int64_t)blockIdx.x * G + wave;
   const int N = a.N;
-  // slot flags [NS·S][64] (rows past N stay 0: the last segment's loads are unguarded)
-  unsigned char* fl = lq_smem + (size_t)wave * a.NS * S * 64;
-  double* ck = a.ck + (size_t)gw * a.NS * 9 * 64;
+  // slot flags [NS·S][64] bytes, or [NS·S/2][64] packed (rows past N stay 0: the last
+  // segment's loads are unguarded)
+  const int fbytes = PK ? a.NS * S / 2 : a.NS * S;
+  const Flags<PK> fl{lq_smem + (size_t)wave * fbytes * 64};
+  double2* rbuf = nullptr;  // PK: next segment's bound rows [S][64]
+  double2* cbuf = nullptr;  // PK: next segment's checkpoint, five 1-KiB pieces
+  if constexpr (PK) {
+    unsigned char* base = lq_smem + (size_t)G * fbytes * 64;
+    rbuf = reinterpret_cast<double2*>(base) + (size_t)wave * (S + 5) * 64;
+    cbuf = rbuf + S * 64;
+  }
+  double* ck = a.ck + (size_t)gw * a.NS * ck_stride<PK>();
   const CkIO<NT> io{};
   int axis;
   int64_t b0;
@@ -518,7 +624,7 @@ __global__ void __launch_bounds__(64 * G, W)
     L.hl = a.hl + off;
   }
   const int jfull = N / S;  // segments [0, jfull) are full
-  for (int k = 0; k < a.NS * S; ++k) fl[k * 64 + lane] = 0;
+  for (int k = 0; k < fbytes; ++k) fl.p[k * 64 + lane] = 0;
 
   double x[3] = {0.0, 0.0, 0.0};
   if (valid) {
@@ -568,11 +674,19 @@ __global__ void __launch_bounds__(64 * G, W)
         Ric v{0, 0, 0, 0, 0, 0, 0, 0, 0};
         SegIn<S> cur;
         SegOut<S> g;
+        if constexpr (PK) glds_rows<S>(a, a.NS - 1, L, i, rbuf);
         // sweep A, free tail: the s recursion, checkpoints of s
 #pragma unroll 1
         for (int j = a.NS - 1; j >= jt; --j) {
-          seg_load<S, false>(a, j, L, i, fl, cur);
-          ck_store_s(io, ck, j, v, lane);
+          if constexpr (PK) {
+            wait_vm0();
+            seg_load_lds<S, false>(j, L, rbuf, fl, cur);
+            wait_lgkm0();
+            if (j > 0) glds_rows<S>(a, j - 1, L, i, rbuf);
+          } else {
+            seg_load<S, false>(a, j, L, i, fl, cur);
+          }
+          ck_store_s<PK>(io, ck, j, v, lane);
           if (j < jfull)
             seg_tail<S, true, false>(a, tab, j, v, cur, g);
           else
@@ -590,8 +704,15 @@ __global__ void __launch_bounds__(64 * G, W)
         // sweep A, working-set segments: full Riccati, checkpoints of (P, s)
 #pragma unroll 1
         for (int j = jt - 1; j >= 0; --j) {
-          seg_load<S, true>(a, j, L, i, fl, cur);
-          ck_store(io, ck, j, v, lane);
+          if constexpr (PK) {
+            wait_vm0();
+            seg_load_lds<S, true>(j, L, rbuf, fl, cur);
+            wait_lgkm0();
+            if (j > 0) glds_rows<S>(a, j - 1, L, i, rbuf);
+          } else {
+            seg_load<S, true>(a, j, L, i, fl, cur);
+          }
+          ck_store<PK>(io, ck, j, v, lane);
           const bool fr = seg_free(cur);
           if (j < jfull) {
             if (fr)
@@ -608,10 +729,42 @@ __global__ void __launch_bounds__(64 * G, W)
         // sweep B: per segment from the front — recompute its steps from the checkpoint,
         // forward, then (working-set segments) the costate back through it
         double xs[3] = {x[0], a.T * x[1], a.Tsq * x[2]};  // ξ
+        if constexpr (PK) {
+          wait_vm0();  // sweep A's checkpoint stores have landed before they are read back
+          glds_rows<S>(a, 0, L, i, rbuf);
+          if (jt > 0)
+            glds_ck(ck, 0, lane, cbuf, 0, 5);
+          else
+            glds_ck(ck, 0, lane, cbuf, 3, 5);
+        }
 #pragma unroll 1
         for (int j = 0; j < jt; ++j) {
-          seg_load<S, true>(a, j, L, i, fl, cur);
-          ck_load(io, ck, j, v, lane);
+          if constexpr (PK) {
+            wait_vm0();
+            seg_load_lds<S, true>(j, L, rbuf, fl, cur);
+            const double2* cb = cbuf + lane;
+            const double2 c0 = cb[0], c1 = cb[64], c2 = cb[128], c3 = cb[192], c4 = cb[256];
+            v.p00 = c0.x;
+            v.p01 = c0.y;
+            v.p02 = c1.x;
+            v.p11 = c1.y;
+            v.p12 = c2.x;
+            v.p22 = c2.y;
+            v.s0 = c3.x;
+            v.s1 = c3.y;
+            v.s2 = c4.x;
+            wait_lgkm0();
+            if (j + 1 < a.NS) {
+              glds_rows<S>(a, j + 1, L, i, rbuf);
+              if (j + 1 < jt)
+                glds_ck(ck, j + 1, lane, cbuf, 0, 5);
+              else
+                glds_ck(ck, j + 1, lane, cbuf, 3, 5);
+            }
+          } else {
+            seg_load<S, true>(a, j, L, i, fl, cur);
+            ck_load(io, ck, j, v, lane);
+          }
           // (a free form here, as in sweep A, costs more registers than it saves)
           if (j < jfull)
             seg_sweep_b<S, true>(a, j, v, cur, g, xs, u0, changed, kl, fl, lane);
@@ -620,8 +773,23 @@ __global__ void __launch_bounds__(64 * G, W)
         }
 #pragma unroll 1
         for (int j = jt; j < a.NS; ++j) {
-          seg_load<S, false>(a, j, L, i, fl, cur);
-          ck_load_s(io, ck, j, v, lane);
+          if constexpr (PK) {
+            wait_vm0();
+            seg_load_lds<S, false>(j, L, rbuf, fl, cur);
+            const double2* cb = cbuf + lane;
+            const double2 c3 = cb[192], c4 = cb[256];
+            v.s0 = c3.x;
+            v.s1 = c3.y;
+            v.s2 = c4.x;
+            wait_lgkm0();
+            if (j + 1 < a.NS) {
+              glds_rows<S>(a, j + 1, L, i, rbuf);
+              glds_ck(ck, j + 1, lane, cbuf, 3, 5);
+            }
+          } else {
+            seg_load<S, false>(a, j, L, i, fl, cur);
+            ck_load_s(io, ck, j, v, lane);
+          }
           if (j < jfull) {
             seg_tail<S, true, true>(a, tab, j, v, cur, g);
             seg_forward_tail<S, true>(a, tab, j, cur, g, xs, u0, changed, kl, fl, lane);
@@ -657,8 +825,22 @@ __global__ void __launch_bounds__(64 * G, W)
         if (i < a.nsteps) {
           // warm start: the converged set shifted one slot towards the present (slot N−1
           // kept), this lane's column only
+          if constexpr (PK) {
+            // nibble pairs: new byte q = (slot 2q+1, slot 2q+2) of the old set
+            const int nb = (N - 1) >> 1;  // bytes fully below slot N−1
+#pragma unroll 4
+            for (int q = 0; q < nb; ++q) {
+              unsigned char* p0 = fl.p + q * 64 + lane;
+              *p0 = (unsigned char)((*p0 >> 4) | ((p0[64] & 0xF) << 4));
+            }
+            if ((N - 1) & 1) {  // slot N−2 (low nibble of byte nb) takes slot N−1
+              unsigned char* p0 = fl.p + nb * 64 + lane;
+              *p0 = (unsigned char)((*p0 & 0xF0) | (*p0 >> 4));
+            }
+          } else {
 #pragma unroll 8
-          for (int k = 0; k < N - 1; ++k) fl[k * 64 + lane] = fl[(k + 1) * 64 + lane];
+            for (int k = 0; k < N - 1; ++k) fl.p[k * 64 + lane] = fl.p[(k + 1) * 64 + lane];
+          }
           klast = (kl >= N - 1) ? N - 1 : max(kl - 1, -1);
         } else {
           active = false;
@@ -761,53 +943,68 @@ hipError_t stage(const double* hi, const double* lo, int64_t sb, int64_t st, int
   return hipGetLastError();
 }
 
-// Kernel variant: Riccati steps per segment S × waves per SIMD W (ZMPC_STRICT_LQ="SxW",
-// A/B only; default below).
+// Kernel variant: Riccati steps per segment S × waves per SIMD W × waves per workgroup G, and
+// PK = segment prefetch through LDS (ZMPC_STRICT_LQ="SxWxG" or "SxWxGp", A/B only; default
+// below).
 struct LqVariant {
   int S, W, G;
+  bool pk;
   void (*kernel)(LqArgs, const double*);     // checkpoints cached (shared CoP, window mode)
   void (*kernel_nt)(LqArgs, const double*);  // checkpoints non-temporal (per-walk bounds)
 };
 
-#define ZMPC_LQV(S, W, G) \
-  {S, W, G, zmpc_strict_lq_kernel<S, W, G, false>, zmpc_strict_lq_kernel<S, W, G, true>}
+#define ZMPC_LQV(S, W, G, PK)                                                             \
+  {S, W, G, PK, zmpc_strict_lq_kernel<S, W, G, false, PK>,                                 \
+   zmpc_strict_lq_kernel<S, W, G, true, PK>}
 const LqVariant kLqVariants[] = {
-    ZMPC_LQV(8, 2, 8),  // default
-    ZMPC_LQV(8, 2, 4),  // N up to 640 (slot flags of 4 waves in LDS)
-    ZMPC_LQV(8, 2, 2),  // N up to 1280
-    ZMPC_LQV(8, 2, 1),  // N up to 2560
-    ZMPC_LQV(6, 2, 8),
-    ZMPC_LQV(8, 1, 8),
-    ZMPC_LQV(4, 3, 4),  // A/B: 3 waves per SIMD (≤ 168 VGPRs), 4-wave workgroups
+    ZMPC_LQV(8, 2, 8, false),  // default
+    ZMPC_LQV(8, 2, 4, false),  // N up to 640 (slot flags of 4 waves in LDS)
+    ZMPC_LQV(8, 2, 2, false),  // N up to 1280
+    ZMPC_LQV(8, 2, 1, false),  // N up to 2560
+    ZMPC_LQV(8, 2, 8, true),   // segment prefetch through LDS
+    ZMPC_LQV(8, 2, 4, true),
+    ZMPC_LQV(6, 2, 8, false),
+    ZMPC_LQV(8, 1, 8, false),
+    ZMPC_LQV(4, 3, 4, false),  // A/B: 3 waves per SIMD (≤ 168 VGPRs), 4-wave workgroups
 };
 #undef ZMPC_LQV
 constexpr size_t kLdsCap = 160 * 1024;
+
+// LDS of one workgroup: the G waves' slot flags (+ PK: their segment buffers).
+size_t lq_lds_bytes(const LqVariant& v, int N) {
+  const size_t rows = (size_t)(N + v.S - 1) / v.S * v.S;
+  const size_t per_wave = v.pk ? rows / 2 * 64 + (size_t)(v.S + 5) * 64 * 16 : rows * 64;
+  return (size_t)v.G * per_wave;
+}
 
 LqVariant lq_variant() {
   static LqVariant v = [] {
     LqVariant d = kLqVariants[0];
     const char* e = getenv("ZMPC_STRICT_LQ");
     if (e) {
-      int s = 0, w = 0, g = 8;  // "SxW" or "SxWxG"
-      if (sscanf(e, "%dx%dx%d", &s, &w, &g) >= 2)
+      int s = 0, w = 0, g = 8;  // "SxW", "SxWxG" or "SxWxGp"
+      const int got = sscanf(e, "%dx%dx%d", &s, &w, &g);
+      const bool pk = strchr(e, 'p') != nullptr;
+      if (got >= 2)
         for (const LqVariant& c : kLqVariants)
-          if (c.S == s && c.W == w && c.G == g) d = c;
+          if (c.S == s && c.W == w && c.G == g && c.pk == pk) d = c;
     }
     return d;
   }();
   return v;
 }
 
-// The configured variant, or — when its G waves' slot flags (G × ⌈N/S⌉·S × 64 bytes) do not
-// fit a CU's LDS — the same S and W with the largest G that fits (N ≤ 2560 at G = 1).
+// The configured variant, or — when its LDS (G waves' slot flags, + PK buffers) does not fit a
+// CU — the same S, W (and PK, then without it) with the largest G that fits (N ≤ 2560 at G = 1).
 LqVariant lq_variant_for(int N) {
   const LqVariant v = lq_variant();
-  const size_t rows = (size_t)(N + v.S - 1) / v.S * v.S;
-  if ((size_t)v.G * rows * 64 <= kLdsCap) return v;
-  for (int g = v.G / 2; g >= 1; g /= 2)
-    for (const LqVariant& c : kLqVariants)
-      if (c.S == v.S && c.W == v.W && c.G == g && (size_t)g * rows * 64 <= kLdsCap) return c;
-  return LqVariant{v.S, v.W, 0, nullptr, nullptr};
+  if (lq_lds_bytes(v, N) <= kLdsCap) return v;
+  for (bool pk : {v.pk, false})
+    for (int g = v.G; g >= 1; g /= 2)
+      for (const LqVariant& c : kLqVariants)
+        if (c.S == v.S && c.W == v.W && c.G == g && c.pk == pk && lq_lds_bytes(c, N) <= kLdsCap)
+          return c;
+  return LqVariant{v.S, v.W, 0, false, nullptr, nullptr};
 }
 
 void fill_consts(const zmpc_plan* p, LqArgs& a) {
@@ -846,7 +1043,7 @@ hipError_t launch_lq(const zmpc_plan* p, LqArgs& a, int64_t waves, hipStream_t s
   static const bool dbg_on = getenv("ZMPC_DEBUG_STRICT") != nullptr;  // diagnostics only
   const LqVariant var = lq_variant_for(p->N);
   const int64_t blocks = (waves + var.G - 1) / var.G;
-  const size_t lds = (size_t)var.G * a.NS * var.S * 64;
+  const size_t lds = lq_lds_bytes(var, p->N);
   // rollouts over per-walk bounds: non-temporal checkpoints (see CkIO)
   const bool nt = !a.window_mode && !a.shared;
   hipLaunchKernelGGL(nt ? var.kernel_nt : var.kernel, dim3((unsigned)blocks), dim3(64 * var.G),
@@ -918,7 +1115,7 @@ hipError_t zmpc_launch_rollout_strict_lq(const zmpc_plan* p, int64_t B, int64_t 
   a.groups = (Bst + 63) / 64;
   a.rows = n + (int64_t)a.NS * lq_variant().S;  // the last segment reads up to NS·S − 1 ahead
   const int64_t G = lq_variant_for(p->N).G;  // checkpoints for every wave of the launched blocks
-  const size_t ck_doubles = (size_t)((waves + G - 1) / G * G) * a.NS * 9 * 64;
+  const size_t ck_doubles = (size_t)((waves + G - 1) / G * G) * a.NS * 10 * 64;  // ≥ either layout
   const size_t st_doubles = (size_t)2 * a.groups * a.rows * 64 * 2;  // 2 axes, (hi, lo)
   double* ws = nullptr;
   if (hipMallocAsync((void**)&ws, (ck_doubles + st_doubles) * sizeof(double), s) != hipSuccess) {
@@ -955,7 +1152,7 @@ hipError_t zmpc_launch_step_strict_lq(const zmpc_plan* p, int64_t B, const doubl
   a.rows = (int64_t)a.NS * lq_variant().S;
   const int64_t waves = (B + 63) / 64;
   const int64_t G = lq_variant_for(p->N).G;  // checkpoints for every wave of the launched blocks
-  const size_t ck_doubles = (size_t)((waves + G - 1) / G * G) * a.NS * 9 * 64;
+  const size_t ck_doubles = (size_t)((waves + G - 1) / G * G) * a.NS * 10 * 64;  // ≥ either layout
   const size_t st_doubles = (size_t)a.groups * a.rows * 64 * 2;  // (hi, lo)
   double* ws = nullptr;
   if (hipMallocAsync((void**)&ws, (ck_doubles + st_doubles) * sizeof(double), s) != hipSuccess) {
