@@ -675,7 +675,7 @@ __global__ void __launch_bounds__(128, 8) zmpc_rollout_unc_axis_kernel(RolloutAr
 // PM (the persistent kernel): the walk's global loads and its history copy-out are issued at
 // raised wave priority, so a CU's co-resident walks get their memory traffic out ahead of the
 // others' correlation (config 2: 45.3 → 43.8 µs; the one-walk-per-workgroup grid is not helped).
-template <int CW, bool SHF = false, bool PM = false>
+template <int CW, bool SHF = false, bool PM = false, int RND = 1>
 __device__ __forceinline__ void split_walk(const RolloutArgs& a, int64_t b, double* smem,
                                            int* flag, const double* __restrict__ kg,
                                            const double* __restrict__ scanP,
@@ -783,52 +783,68 @@ __device__ __forceinline__ void split_walk(const RolloutArgs& a, int64_t b, doub
     x[i] = (lane == 0) ? xi[i] : p;
   }
   // ---- 5. replay (reference form) straight into the staged history ------------------------
+  // RND = 2 (A/B): the rows go out in two rounds of ⌈n/2⌉ through half the LDS (more walks
+  // resident per CU), the cheap replay recomputed per round
   double* stage = smem;
-  if (lane == 0) {
-    stage[3 * axis + 0] = xi[0];
-    stage[3 * axis + 1] = xi[1];
-    stage[3 * axis + 2] = xi[2];
-  }
+  const int rows_per_round = (n + RND - 1) / RND;
+  const double xs0[3] = {x[0], x[1], x[2]};
 #pragma unroll
-  for (int q = 0; q < CW; ++q) {
-    const int m = mbeg + q;
-    if (m < nsteps) {
-      const double u = f[q] - (kx0 * x[0] + kx1 * x[1] + kx2 * x[2]);
-      double xn[3];
-      lipm_step(lc, x, u, xn);
-      if (m == kick_step) xn[1] -= kk;
-      double* o = stage + (m + 1) * 6 + 3 * axis;
-      o[0] = xn[0];
-      o[1] = xn[1];
-      o[2] = xn[2];
+  for (int rnd = 0; rnd < RND; ++rnd) {
+    const int r0 = rnd * rows_per_round, r1 = min(n, r0 + rows_per_round);
+    if (RND > 1) {
 #pragma unroll
-      for (int i = 0; i < 3; ++i) x[i] = xn[i];
+      for (int i = 0; i < 3; ++i) x[i] = xs0[i];
     }
-  }
-  if (a.status != nullptr) {
-    const bool finite = isfinite(x[0]) && isfinite(x[1]) && isfinite(x[2]);
-    const unsigned long long bad = __ballot(!finite);
-    if (lane == 0) flag[axis] = bad ? ZMPC_ST_NONFINITE : 0;
-  }
-  __syncthreads();
-  // ---- 6. coalesced copy-out ---------------------------------------------------------------
-  if (!(a.dbg & 4)) {
-    if constexpr (PM) __builtin_amdgcn_s_setprio(3);
-    const double2* src = reinterpret_cast<const double2*>(stage);
-    double2* dst = reinterpret_cast<double2*>(hist + b * (int64_t)n * 6);
-    // four rows in flight per thread (LDS reads batched ahead of the stores); the history is
-    // written once and never re-read here: non-temporal stores (config 4 unconstrained
-    // 0.547 → 0.497 ms in an A/B on one box; config 2 unchanged)
-    int e = tid;
-    for (; e + 3 * 128 < n * 3; e += 4 * 128) {
-      const double2 v0 = src[e], v1 = src[e + 128], v2 = src[e + 256], v3 = src[e + 384];
-      st_nt2(&dst[e], v0);
-      st_nt2(&dst[e + 128], v1);
-      st_nt2(&dst[e + 256], v2);
-      st_nt2(&dst[e + 384], v3);
+    if (lane == 0 && r0 == 0) {
+      stage[3 * axis + 0] = xi[0];
+      stage[3 * axis + 1] = xi[1];
+      stage[3 * axis + 2] = xi[2];
     }
-    for (; e < n * 3; e += 128) st_nt2(&dst[e], src[e]);
-    if constexpr (PM) __builtin_amdgcn_s_setprio(0);
+#pragma unroll
+    for (int q = 0; q < CW; ++q) {
+      const int m = mbeg + q;
+      if (m < nsteps) {
+        const double u = f[q] - (kx0 * x[0] + kx1 * x[1] + kx2 * x[2]);
+        double xn[3];
+        lipm_step(lc, x, u, xn);
+        if (m == kick_step) xn[1] -= kk;
+        if (RND == 1 || (m + 1 >= r0 && m + 1 < r1)) {
+          double* o = stage + (m + 1 - r0) * 6 + 3 * axis;
+          o[0] = xn[0];
+          o[1] = xn[1];
+          o[2] = xn[2];
+        }
+#pragma unroll
+        for (int i = 0; i < 3; ++i) x[i] = xn[i];
+      }
+    }
+    if (rnd == RND - 1 && a.status != nullptr) {
+      const bool finite = isfinite(x[0]) && isfinite(x[1]) && isfinite(x[2]);
+      const unsigned long long bad = __ballot(!finite);
+      if (lane == 0) flag[axis] = bad ? ZMPC_ST_NONFINITE : 0;
+    }
+    __syncthreads();
+    // ---- 6. coalesced copy-out ---------------------------------------------------------------
+    if (!(a.dbg & 4)) {
+      if constexpr (PM) __builtin_amdgcn_s_setprio(3);
+      const double2* src = reinterpret_cast<const double2*>(stage);
+      double2* dst = reinterpret_cast<double2*>(hist + b * (int64_t)n * 6 + (int64_t)r0 * 6);
+      const int ne = (r1 - r0) * 3;
+      // four rows in flight per thread (LDS reads batched ahead of the stores); the history is
+      // written once and never re-read here: non-temporal stores (config 4 unconstrained
+      // 0.547 → 0.497 ms in an A/B on one box; config 2 unchanged)
+      int e = tid;
+      for (; e + 3 * 128 < ne; e += 4 * 128) {
+        const double2 v0 = src[e], v1 = src[e + 128], v2 = src[e + 256], v3 = src[e + 384];
+        st_nt2(&dst[e], v0);
+        st_nt2(&dst[e + 128], v1);
+        st_nt2(&dst[e + 256], v2);
+        st_nt2(&dst[e + 384], v3);
+      }
+      for (; e < ne; e += 128) st_nt2(&dst[e], src[e]);
+      if constexpr (PM) __builtin_amdgcn_s_setprio(0);
+    }
+    if (RND > 1 && rnd + 1 < RND) __syncthreads();  // staging read out before the next round
   }
   if (a.status != nullptr && tid == 0) a.status[b] = flag[0] | flag[1];
 }
@@ -875,6 +891,195 @@ __global__ void __launch_bounds__(128, 4)
   for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x) {
     split_walk<CW, SHF, true>(a, b, smem, flag, kg, scanP, kxp, hist);
     __syncthreads();  // staging read out before the next walk's z_ref overwrites it
+  }
+}
+
+// Variant 11 (A/B): the persistent split kernel with the history copied out in two rounds, so
+// a walk needs max(z_ref, half the history) of LDS and 12 walks are resident per CU (84 VGPRs,
+// six waves per SIMD) instead of 8.
+template <int CW>
+__global__ void __launch_bounds__(128, 6)
+    zmpc_rollout_unc_pers2_kernel(RolloutArgs a, const double* __restrict__ kg,
+                                  const double* __restrict__ scanP,
+                                  const double* __restrict__ kxp, double* __restrict__ hist) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  __shared__ int flag[2];
+  for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x) {
+    split_walk<CW, false, true, 2>(a, b, smem, flag, kg, scanP, kxp, hist);
+    __syncthreads();
+  }
+}
+
+// Variant 12 (A/B): the same two-round copy-out, one walk per workgroup.
+template <int CW>
+__global__ void __launch_bounds__(128, 6) zmpc_rollout_unc_split2_kernel(RolloutArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  __shared__ int flag[2];
+  split_walk<CW, false, false, 2>(a, blockIdx.x, smem, flag, a.k, a.scanP, a.kx, a.hist);
+}
+
+// ---- independent axes (A/B variants 9, 10) ---------------------------------------------------
+// The two waves of a walk never wait for each other before the end of the walk: each loads only
+// its axis's bounds (8-byte loads; the partner's loads of the same lines hit in L2), stages its
+// own z_ref, correlates, scans, replays into its own LDS rows (3 doubles per timestep, aliasing
+// its z_ref area) and copies them out with 8-byte stores into its half of each 48-byte history
+// row (the partner fills the other half; both halves meet in L2).  One barrier per walk, for the
+// walk's status.  LDS per wave: max(lzp, 3n) doubles.
+template <int CW>
+__device__ __forceinline__ void indep_walk(const RolloutArgs& a, int64_t b, double* smem,
+                                           int* flag, const double* __restrict__ kg,
+                                           const double* __restrict__ scanP,
+                                           const double* __restrict__ kxp,
+                                           double* __restrict__ hist, int region) {
+  using ZL = ZrLayout<CW>;
+  constexpr int PF = CW + 1;  // 64·(CW+1) >= n for a single-pass walk
+  const int tid = threadIdx.x, lane = tid & 63, axis = tid >> 6;
+  const int n = a.n, nsteps = n - 1;
+  double* zr = smem + (size_t)axis * region;
+  const double* xb = a.x0 + b * 6 + 3 * axis;
+  const double xi[3] = {xb[0], xb[1], xb[2]};
+  const double kk = (axis == 1 && a.kick != nullptr) ? a.kick[b] : 0.0;
+  // ---- 1. this axis's bounds → z_ref (zmp_controller.py:184,197) + window padding (:81-88)
+  {
+    const double* zmx = a.zmax + b * a.bstride + axis;
+    const double* zmn = a.zmin + b * a.bstride + axis;
+    double hi[PF], lo[PF];
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      const int tc = min(u * 64 + lane, n - 1);  // clamped (no predicated loads)
+      hi[u] = zmx[2 * tc];
+      lo[u] = zmn[2 * tc];
+    }
+    double last = 0.0;
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      const int t = u * 64 + lane;
+      const double v = (hi[u] + lo[u]) / 2;
+      if (t < n) zr[ZL::idx(t)] = v;
+      if (u == ((n - 1) >> 6)) last = v;
+    }
+    last = __shfl(last, (n - 1) & 63, 64);
+    for (int t = n + lane; t < a.lz; t += 64) zr[ZL::idx(t)] = last;
+  }
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's z_ref writes are in LDS
+  __builtin_amdgcn_wave_barrier();
+  double f[CW];
+  axis_correlate<CW>(a, kg, zr, lane, f);
+  // ---- 2. lane-chunk affine scan (as split_walk) ----------------------------------------------
+  const int64_t kick_step = (axis == 1) ? kick_step_of(a, b) : -1;
+  const LipmConsts lc = a.lc;
+  const double kx0 = kxp[0], kx1 = kxp[1], kx2 = kxp[2];
+  const double Bv[3] = {lc.T3_6, lc.T2_2, lc.T};
+  Mat3 Ab;
+  {
+    const double A[9] = {1.0, lc.T, lc.T2_2, 0.0, 1.0, lc.T, 0.0, 0.0, 1.0};
+    const double kx[3] = {kx0, kx1, kx2};
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) Ab.m[3 * i + j] = A[3 * i + j] - Bv[i] * kx[j];
+  }
+  const int mbeg = lane * CW;
+  double sv[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+  for (int q = 0; q < CW; ++q) {
+    if (mbeg + q < nsteps) {
+      double t[3];
+      matvec3(Ab, sv, t);
+      sv[0] = fma(Bv[0], f[q], t[0]);
+      sv[1] = fma(Bv[1], f[q], t[1]);
+      sv[2] = fma(Bv[2], f[q], t[2]);
+      if (mbeg + q == kick_step) sv[1] -= kk;
+    }
+  }
+  const double* Pp = scanP + (CW - 1) * kScanStride;
+  if (lane == 0) {
+    double t[3];
+    Mat3 P;
+#pragma unroll
+    for (int q = 0; q < 9; ++q) P.m[q] = Pp[q];
+    matvec3(P, xi, t);
+    for (int i = 0; i < 3; ++i) sv[i] += t[i];
+  }
+#pragma unroll
+  for (int r2 = 0; r2 < 6; ++r2) {
+    const int d = 1 << r2;
+    double u[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) u[i] = __shfl_up(sv[i], d, 64);
+    if (lane >= d) {
+      Mat3 Pd;
+#pragma unroll
+      for (int q = 0; q < 9; ++q) Pd.m[q] = Pp[r2 * 9 + q];
+      double t[3];
+      matvec3(Pd, u, t);
+      for (int i = 0; i < 3; ++i) sv[i] += t[i];
+    }
+  }
+  double x[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const double p = __shfl_up(sv[i], 1, 64);
+    x[i] = (lane == 0) ? xi[i] : p;
+  }
+  // ---- 3. replay (reference form) into this wave's rows (aliasing its dead z_ref) ------------
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_wave_barrier();
+  double* stage = zr;
+  if (lane == 0) {
+    stage[0] = xi[0];
+    stage[1] = xi[1];
+    stage[2] = xi[2];
+  }
+#pragma unroll
+  for (int q = 0; q < CW; ++q) {
+    const int m = mbeg + q;
+    if (m < nsteps) {
+      const double u = f[q] - (kx0 * x[0] + kx1 * x[1] + kx2 * x[2]);
+      double xn[3];
+      lipm_step(lc, x, u, xn);
+      if (m == kick_step) xn[1] -= kk;
+      double* o = stage + (m + 1) * 3;
+      o[0] = xn[0];
+      o[1] = xn[1];
+      o[2] = xn[2];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) x[i] = xn[i];
+    }
+  }
+  const bool finite = isfinite(x[0]) && isfinite(x[1]) && isfinite(x[2]);
+  const unsigned long long bad = __ballot(!finite);
+  __builtin_amdgcn_s_waitcnt(0xC07F);
+  __builtin_amdgcn_wave_barrier();
+  // ---- 4. copy-out: element e = 3·row + c of this axis → hist[b, row, axis, c] ---------------
+  {
+    double* hb = hist + b * (int64_t)n * 6 + 3 * axis;
+    int row = lane / 3, c = lane - 3 * row;  // e = lane, advancing by 64 = 21 rows + 1
+    for (int e = lane; e < 3 * n; e += 64) {
+      hb[row * 6 + c] = stage[e];
+      row += 21;
+      c += 1;
+      if (c == 3) {
+        c = 0;
+        ++row;
+      }
+    }
+  }
+  if (lane == 0) flag[axis] = bad ? ZMPC_ST_NONFINITE : 0;
+}
+
+template <int CW, bool PERS>
+__global__ void __launch_bounds__(128, 4)
+    zmpc_rollout_unc_indep_kernel(RolloutArgs a, const double* __restrict__ kg,
+                                  const double* __restrict__ scanP,
+                                  const double* __restrict__ kxp, double* __restrict__ hist,
+                                  int region) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  __shared__ int flag[2];
+  for (int64_t b = blockIdx.x; b < a.B; b += PERS ? gridDim.x : a.B) {
+    indep_walk<CW>(a, b, smem, flag, kg, scanP, kxp, hist, region);
+    __syncthreads();
+    if (a.status != nullptr && threadIdx.x == 0) a.status[b] = flag[0] | flag[1];
   }
 }
 
@@ -1523,6 +1728,43 @@ void launch_unc(const RolloutGeom& g, size_t lds, hipStream_t s, const RolloutAr
     const size_t lds_h = 6 * (size_t)a.n * sizeof(double);
     hipLaunchKernelGGL((zmpc_rollout_unc_split_kernel<CW, true>), dim3((unsigned)a.B), dim3(128),
                        lds_h, s, a);
+    return;
+  }
+  if (g.passes == 1 && variant == 12) {
+    const size_t lds_h = std::max<size_t>(lds_axis, 6 * (size_t)((a.n + 1) / 2) * sizeof(double));
+    hipLaunchKernelGGL(zmpc_rollout_unc_split2_kernel<CW>, dim3((unsigned)a.B), dim3(128), lds_h,
+                       s, a);
+    return;
+  }
+  if (g.passes == 1 && variant == 11) {
+    const size_t lds_h = std::max<size_t>(lds_axis, 6 * (size_t)((a.n + 1) / 2) * sizeof(double));
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per_cu, reinterpret_cast<const void*>(zmpc_rollout_unc_pers2_kernel<CW>), 128,
+            lds_h) != hipSuccess)
+      per_cu = 0;
+    const int64_t grid = (int64_t)std::max(g_cus, 1) * std::max(per_cu, 1);
+    hipLaunchKernelGGL(zmpc_rollout_unc_pers2_kernel<CW>,
+                       dim3((unsigned)std::min<int64_t>(grid, a.B)), dim3(128), lds_h, s, a, a.k,
+                       a.scanP, a.kx, a.hist);
+    return;
+  }
+  if (g.passes == 1 && (variant == 9 || variant == 10)) {
+    // A/B: independent axes (indep_walk), persistent (9) or one walk per workgroup (10)
+    const int region = (int)std::max<int64_t>(a.lzp, 3 * (int64_t)a.n + 1) & ~1;
+    const size_t lds_i = 2 * (size_t)(region + 2) * sizeof(double);
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per_cu, reinterpret_cast<const void*>(zmpc_rollout_unc_indep_kernel<CW, true>), 128,
+            lds_i) != hipSuccess)
+      per_cu = 0;
+    const int64_t grid = (int64_t)std::max(g_cus, 1) * std::max(per_cu, 1);
+    if (variant == 9 && grid < a.B)
+      hipLaunchKernelGGL((zmpc_rollout_unc_indep_kernel<CW, true>), dim3((unsigned)grid),
+                         dim3(128), lds_i, s, a, a.k, a.scanP, a.kx, a.hist, region + 2);
+    else
+      hipLaunchKernelGGL((zmpc_rollout_unc_indep_kernel<CW, false>), dim3((unsigned)a.B),
+                         dim3(128), lds_i, s, a, a.k, a.scanP, a.kx, a.hist, region + 2);
     return;
   }
   if (g.passes == 1 && (variant == 8 || variant == 6) && lds_split <= 64 * 1024) {
