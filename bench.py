@@ -101,13 +101,13 @@ def rollout_kernel_name(B, n, N, strict, shared=False):
     if strict:
         return "zmpc_strict_lq_kernel"
     if shared and n - 1 <= 512 and 6 * n * 8 <= 64 * 1024:
-        return "zmpc_rollout_unc_split_kernel<CW, true> (+ zmpc_shared_f_kernel)"
+        return "zmpc_rollout_unc_splitd_kernel<CW, true> (+ zmpc_shared_f_kernel)"
     if fft_transform(n, N):
         return "zmpc_rollout_unc_wide_kernel<CW, W, E> (FFT correlation)"
     if n - 1 <= 512:
         slots = 8 * torch.cuda.get_device_properties(0).multi_processor_count
-        return ("zmpc_rollout_unc_pers_kernel" if slots < B <= 3 * slots
-                else "zmpc_rollout_unc_split_kernel")
+        return ("zmpc_rollout_unc_persd_kernel" if slots < B <= 3 * slots
+                else "zmpc_rollout_unc_splitd_kernel")
     return "zmpc_rollout_unc_wide_kernel" if n - 1 <= 4096 else "zmpc_rollout_unc_chunk_kernel"
 
 

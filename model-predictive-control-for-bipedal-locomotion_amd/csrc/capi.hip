@@ -125,7 +125,7 @@ int zmpc_plan_create(int device, int32_t N, double T, double T2_2, double T3_6, 
     double** ptr;
     size_t n;
   } allocs[] = {{&P->p, (size_t)N},  {&P->Px, 3 * (size_t)N}, {&P->M, nn}, {&P->L, nn},
-                {&P->k, (size_t)P->Kpad + 64}, {&P->kx, 4}, {&P->scanP, 8 * kScanStride},
+                {&P->k, (size_t)P->Kpad + 64}, {&P->kx, 4}, {&P->scanP, kScanDoubles},
                 {&P->X, strict ? nn : 0}, {&P->G, strict ? nn : 0},
                 {&P->v, strict ? (size_t)N : 0}, {&P->Hz, strict ? nn : 0},
                 {&P->fft_tw, 2 * (size_t)kFftPT}, {&P->fft_g, 2 * (size_t)kFftGComplex}};

@@ -334,6 +334,16 @@ __global__ void zmpc_scan_matrices(double T, double T2_2, double T3_6,
       mul(P, Ab, t);
       for (int q = 0; q < 9; ++q) P[q] = t[q];
     }
+    // per-lane powers (Ā^C)^k, k = 0..32
+    {
+      double W[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+      for (int k = 0; k <= 32; ++k) {
+        for (int q = 0; q < 9; ++q) out[kScanPowOff + ((C - 1) * 33 + k) * 9 + q] = W[q];
+        double t[9];
+        mul(W, P, t);
+        for (int q = 0; q < 9; ++q) W[q] = t[q];
+      }
+    }
     double Q[9];
     for (int q = 0; q < 9; ++q) Q[q] = P[q];
     for (int r = 0; r < kScanLevels; ++r) {

@@ -52,6 +52,62 @@ __device__ __forceinline__ void matvec3(const Mat3& a, const double* x, double* 
     y[i] = fma(a.m[3 * i + 0], x[0], fma(a.m[3 * i + 1], x[1], a.m[3 * i + 2] * x[2]));
 }
 
+// A double moved across lanes by DPP (two 32-bit halves); `ctrl` a DPP control word,
+// row_mask the rows written (the others keep 0), out-of-row reads 0 (bound_ctrl).
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, ROWS, 0xF, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, ROWS, 0xF, true);
+  return __hiloint2double(hi, lo);
+}
+
+// Inclusive affine Kogge-Stone scan over the 64 lanes, T_l = Σ_{m≤l} P^(l−m) s_m, on the VALU's
+// DPP lane moves instead of LDS-pipe shuffles: four row_shr levels (1, 2, 4, 8) inside each
+// 16-lane row with the uniform P^(2^r), then row_bcast:15 (rows 1, 3 take lanes 15, 47) and
+// row_bcast:31 (rows 2, 3 take lane 31) with each lane's own power P^k from the plan
+// (pw = [33][9], k = its distance to the source lane).
+__device__ __forceinline__ void dpp_level(double* sv, const Mat3& M, double u0, double u1,
+                                          double u2) {
+  const double u[3] = {u0, u1, u2};
+  double t[3];
+  matvec3(M, u, t);
+  sv[0] += t[0];
+  sv[1] += t[1];
+  sv[2] += t[2];
+}
+
+__device__ __forceinline__ void scan_dpp(double* sv, int lane, const double* __restrict__ Pp,
+                                         const double* __restrict__ pw) {
+#define ZMPC_DPP_ROW(R2, CTRL)                                                             \
+  {                                                                                        \
+    Mat3 Pd;                                                                               \
+    _Pragma("unroll") for (int q = 0; q < 9; ++q) Pd.m[q] = Pp[(R2) * 9 + q];              \
+    dpp_level(sv, Pd, dpp_f64<CTRL, 0xF>(sv[0]), dpp_f64<CTRL, 0xF>(sv[1]),                \
+              dpp_f64<CTRL, 0xF>(sv[2]));                                                  \
+  }
+  ZMPC_DPP_ROW(0, 0x111)  // row_shr:1
+  ZMPC_DPP_ROW(1, 0x112)  // row_shr:2
+  ZMPC_DPP_ROW(2, 0x114)  // row_shr:4
+  ZMPC_DPP_ROW(3, 0x118)  // row_shr:8
+#undef ZMPC_DPP_ROW
+  {  // rows 1 and 3 take lane 15 / 47 at distance (lane & 15) + 1
+    const double* m = pw + ((lane & 15) + 1) * 9;
+    Mat3 M;
+#pragma unroll
+    for (int q = 0; q < 9; ++q) M.m[q] = m[q];
+    dpp_level(sv, M, dpp_f64<0x142, 0xA>(sv[0]), dpp_f64<0x142, 0xA>(sv[1]),
+              dpp_f64<0x142, 0xA>(sv[2]));
+  }
+  {  // rows 2 and 3 take lane 31 at distance lane − 31
+    const double* m = pw + (lane >= 32 ? lane - 31 : 0) * 9;
+    Mat3 M;
+#pragma unroll
+    for (int q = 0; q < 9; ++q) M.m[q] = m[q];
+    dpp_level(sv, M, dpp_f64<0x143, 0xC>(sv[0]), dpp_f64<0x143, 0xC>(sv[1]),
+              dpp_f64<0x143, 0xC>(sv[2]));
+  }
+}
+
 // Reference state update x⁺ = A x + B u (zmp_controller.py:199).
 __device__ __forceinline__ void lipm_step(const LipmConsts& c, const double* x, double u,
                                           double* y) {
@@ -675,7 +731,7 @@ __global__ void __launch_bounds__(128, 8) zmpc_rollout_unc_axis_kernel(RolloutAr
 // PM (the persistent kernel): the walk's global loads and its history copy-out are issued at
 // raised wave priority, so a CU's co-resident walks get their memory traffic out ahead of the
 // others' correlation (config 2: 45.3 → 43.8 µs; the one-walk-per-workgroup grid is not helped).
-template <int CW, bool SHF = false, bool PM = false, int RND = 1>
+template <int CW, bool SHF = false, bool PM = false, int RND = 1, bool DPP = false>
 __device__ __forceinline__ void split_walk(const RolloutArgs& a, int64_t b, double* smem,
                                            int* flag, const double* __restrict__ kg,
                                            const double* __restrict__ scanP,
@@ -760,10 +816,11 @@ __device__ __forceinline__ void split_walk(const RolloutArgs& a, int64_t b, doub
     matvec3(P, xi, t);
     for (int i = 0; i < 3; ++i) sv[i] += t[i];
   }
+  if constexpr (DPP) scan_dpp(sv, lane, Pp, scanP + kScanPowOff + (CW - 1) * 33 * 9);
 #pragma unroll
   for (int r2 = 0; r2 < 6; ++r2) {
     const int d = 1 << r2;
-    if (a.dbg & 2) break;
+    if (DPP || (a.dbg & 2)) break;
     double u[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) u[i] = __shfl_up(sv[i], d, 64);
@@ -892,6 +949,32 @@ __global__ void __launch_bounds__(128, 4)
     split_walk<CW, SHF, true>(a, b, smem, flag, kg, scanP, kxp, hist);
     __syncthreads();  // staging read out before the next walk's z_ref overwrites it
   }
+}
+
+// The persistent split kernel with the DPP lane scan (scan_dpp): the default for config-2
+// shaped batches (variant 8; variant 15 = zmpc_rollout_unc_pers_kernel, the shuffle scan).
+template <int CW>
+__global__ void __launch_bounds__(128, 4)
+    zmpc_rollout_unc_persd_kernel(RolloutArgs a, const double* __restrict__ kg,
+                                  const double* __restrict__ scanP,
+                                  const double* __restrict__ kxp, double* __restrict__ hist) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  __shared__ int flag[2];
+  // (the tables through the argument struct: as __restrict__ arguments they go to SGPRs and
+  // the DPP scan's per-lane powers push the kernel into spills)
+  for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x) {
+    split_walk<CW, false, true, 1, true>(a, b, smem, flag, a.k, a.scanP, a.kx, a.hist);
+    __syncthreads();
+  }
+}
+
+// One walk per workgroup with the DPP lane scan (variant 6 and large batches of variant 8;
+// variant 16 = zmpc_rollout_unc_split_kernel, the shuffle scan).
+template <int CW, bool SHF = false>
+__global__ void __launch_bounds__(128, 4) zmpc_rollout_unc_splitd_kernel(RolloutArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  __shared__ int flag[2];
+  split_walk<CW, SHF, false, 1, true>(a, blockIdx.x, smem, flag, a.k, a.scanP, a.kx, a.hist);
 }
 
 // Variant 11 (A/B): the persistent split kernel with the history copied out in two rounds, so
@@ -1714,8 +1797,10 @@ template <int CW>
 void launch_unc(const RolloutGeom& g, size_t lds, hipStream_t s, const RolloutArgs& a) {
   // Kernel choice; ZMPC_ROLLOUT_VARIANT overrides it for A/B runs (DESIGN.md §4 has the
   // config-2 measurements): 8 = split, persistent grid (default); 6 = split, one walk per
-  // workgroup; 1 = split-axis at 16 walks per CU staging through the z_ref area; 2 = one wave
-  // per walk.  All single-pass kernels produce identical histories (tests/test_gpu_parity.py).
+  // workgroup (both with the DPP lane scan; 15 / 16 the same with the shuffle scan); 1 =
+  // split-axis at 16 walks per CU staging through the z_ref area; 2 = one wave per walk;
+  // 9 / 10 independent axes; 11 / 12 two-round copy-out.  All single-pass kernels produce the
+  // same histories to rounding (tests/test_gpu_parity.py).
   static const int variant = [] {
     const char* e = getenv("ZMPC_ROLLOUT_VARIANT");
     return e ? atoi(e) : 8;
@@ -1724,10 +1809,15 @@ void launch_unc(const RolloutGeom& g, size_t lds, hipStream_t s, const RolloutAr
   const size_t lds_split = std::max<size_t>(lds_axis, 6 * (size_t)a.n * sizeof(double));
   RolloutArgs b = a;
   if (a.fsh != nullptr) {
-    // shared CoP, f precomputed: scan, replay and the history stores only
+    // shared CoP, f precomputed: scan (DPP; variant 16: shuffles), replay and the history
+    // stores only
     const size_t lds_h = 6 * (size_t)a.n * sizeof(double);
-    hipLaunchKernelGGL((zmpc_rollout_unc_split_kernel<CW, true>), dim3((unsigned)a.B), dim3(128),
-                       lds_h, s, a);
+    if (variant == 16)
+      hipLaunchKernelGGL((zmpc_rollout_unc_split_kernel<CW, true>), dim3((unsigned)a.B),
+                         dim3(128), lds_h, s, a);
+    else
+      hipLaunchKernelGGL((zmpc_rollout_unc_splitd_kernel<CW, true>), dim3((unsigned)a.B),
+                         dim3(128), lds_h, s, a);
     return;
   }
   if (g.passes == 1 && variant == 12) {
@@ -1767,12 +1857,17 @@ void launch_unc(const RolloutGeom& g, size_t lds, hipStream_t s, const RolloutAr
                          dim3(128), lds_i, s, a, a.k, a.scanP, a.kx, a.hist, region + 2);
     return;
   }
-  if (g.passes == 1 && (variant == 8 || variant == 6) && lds_split <= 64 * 1024) {
+  if (g.passes == 1 && (variant == 8 || variant == 6 || variant == 15 || variant == 16) &&
+      lds_split <= 64 * 1024) {
+    // 8 / 6: the lane scan on DPP moves (scan_dpp; round 3: one walk per workgroup 47.9 → 43.5
+    // µs at B = 4096, 94 → 87 µs at B = 8192, persistent 43.9 → 42.9 µs); 15 / 16: the same
+    // kernels with the round-2 shuffle scan (A/B)
+    const bool dpp = variant == 8 || variant == 6;
+    const void* pk = dpp ? reinterpret_cast<const void*>(zmpc_rollout_unc_persd_kernel<CW>)
+                         : reinterpret_cast<const void*>(zmpc_rollout_unc_pers_kernel<CW>);
     int per_cu = 0;
-    if (variant == 8 &&
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &per_cu, reinterpret_cast<const void*>(zmpc_rollout_unc_pers_kernel<CW>), 128,
-            lds_split) != hipSuccess)
+    if ((variant == 8 || variant == 15) &&
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pk, 128, lds_split) != hipSuccess)
       per_cu = 0;
     static const int per_cu_env = [] {
       const char* e = getenv("ZMPC_PERS_PER_CU");  // A/B only: resident workgroups per CU
@@ -1783,8 +1878,15 @@ void launch_unc(const RolloutGeom& g, size_t lds, hipStream_t s, const RolloutAr
     // persistent only for a few walks per workgroup: config 2 (2 per workgroup) 45 µs vs
     // 49 µs; at 8 per workgroup (B = 16384) the one-walk grid is faster (156 vs 177 µs)
     if (per_cu > 0 && grid < a.B && a.B <= 3 * grid) {
-      hipLaunchKernelGGL(zmpc_rollout_unc_pers_kernel<CW>, dim3((unsigned)grid), dim3(128),
-                         lds_split, s, a, a.k, a.scanP, a.kx, a.hist);
+      if (dpp)
+        hipLaunchKernelGGL(zmpc_rollout_unc_persd_kernel<CW>, dim3((unsigned)grid), dim3(128),
+                           lds_split, s, a, a.k, a.scanP, a.kx, a.hist);
+      else
+        hipLaunchKernelGGL(zmpc_rollout_unc_pers_kernel<CW>, dim3((unsigned)grid), dim3(128),
+                           lds_split, s, a, a.k, a.scanP, a.kx, a.hist);
+    } else if (dpp) {
+      hipLaunchKernelGGL(zmpc_rollout_unc_splitd_kernel<CW>, dim3((unsigned)a.B), dim3(128),
+                         lds_split, s, a);
     } else {
       hipLaunchKernelGGL(zmpc_rollout_unc_split_kernel<CW>, dim3((unsigned)a.B), dim3(128),
                          lds_split, s, a);

@@ -14,6 +14,10 @@
 // (64-lane Kogge-Stone rounds use r <= 5; the 128-lane kernels' cross-wave offset uses r = 6).
 constexpr int kScanLevels = 7;
 constexpr int kScanStride = kScanLevels * 9;
+// ... followed by the per-lane powers (Ā^C)^k, k = 0..32, [8][33][9] (the DPP scan's cross-row
+// steps, rollout.hip scan_dpp)
+constexpr int kScanPowOff = 8 * kScanStride;
+constexpr int kScanDoubles = kScanPowOff + 8 * 33 * 9;
 
 // Longest strict horizon: the LQ kernel's per-wave slot flags ([N][64] bytes) must fit a CU's
 // LDS for one wave per workgroup (strict_lq.hip lq_variant_for).
@@ -39,7 +43,8 @@ struct zmpc_plan {
   double* L = nullptr;   // [N,N] lower Cholesky factor of M
   double* k = nullptr;   // [Kpad] gain row e0ᵀ M⁻¹ Puᵀ (zero-padded)
   double* kx = nullptr;  // [3]  k·Px
-  double* scanP = nullptr;  // [8][kScanLevels][9] (Ā^C)^(2^r) rollout scan propagators
+  double* scanP = nullptr;  // [8][kScanLevels][9] (Ā^C)^(2^r) rollout scan propagators, then
+                            // [8][33][9] (Ā^C)^k (kScanPowOff)
   double* X = nullptr;   // [N,N] L⁻¹ Puᵀ (strict plans)
   double* G = nullptr;   // [N,N] Pu (R I + Q PuᵀPu)⁻¹ Puᵀ (strict plans)
   double* v = nullptr;   // [N]   first column of Pu⁻¹ (strict plans)

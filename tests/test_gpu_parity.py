@@ -413,7 +413,8 @@ np.save(sys.argv[3], h.cpu().numpy())
 
 def test_rollout_kernel_variants_agree(tmp_path):
     """The single-pass kernels (ZMPC_ROLLOUT_VARIANT 8 split persistent — the default, 6 split
-    one walk per workgroup, 1 split-axis with z_ref-area staging, 2 one wave per walk, 9/10
+    one walk per workgroup, both with the DPP lane scan, 15 / 16 the same with the shuffle scan,
+    1 split-axis with z_ref-area staging, 2 one wave per walk, 9/10
     independent axes persistent / one walk per workgroup, 11 / 12 persistent / one walk per workgroup with a two-round
     copy-out) agree."""
     import subprocess
@@ -424,7 +425,7 @@ def test_rollout_kernel_variants_agree(tmp_path):
     inp = tmp_path / "in.npz"
     np.savez(inp, zmax=zmax, zmin=zmin, x0=x0, kick=kick, ks=n // 2, dt=dt)
     outs = []
-    for v in (8, 6, 1, 2, 9, 10, 11, 12):
+    for v in (8, 6, 15, 16, 1, 2, 9, 10, 11, 12):
         out = tmp_path / f"h{v}.npy"
         env = dict(os.environ, ZMPC_ROLLOUT_VARIANT=str(v))
         subprocess.run([sys.executable, "-c", _VARIANT_CHILD, PKG, str(inp), str(out)],
