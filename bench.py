@@ -105,6 +105,11 @@ def rollout_kernel_name(B, n, N, strict, shared=False):
     if fft_transform(n, N):
         return "zmpc_rollout_unc_wide_kernel<CW, W, E> (FFT correlation)"
     if n - 1 <= 512:
+        # chunk width as rollout.hip:pick_cw; odd widths take the fast-FIR correlation, one walk
+        # per workgroup
+        cw = min(range(8, 0, -1), key=lambda c: (-(-(n - 1) // (64 * c)) * c, -c))
+        if cw % 2 == 1:
+            return "zmpc_rollout_unc_splitd_kernel"
         slots = 8 * torch.cuda.get_device_properties(0).multi_processor_count
         return ("zmpc_rollout_unc_persd_kernel" if slots < B <= 3 * slots
                 else "zmpc_rollout_unc_splitd_kernel")

@@ -211,6 +211,20 @@ __global__ void __launch_bounds__(64) zmpc_chol_panel(int N, int p0, const doubl
   }
 }
 
+// 4b. the rollout's two-parallel fast-FIR taps (rollout.hip, axis_correlate_ffa): row m holds
+// (E_m, O_m, E_m + O_{m−1}, 0) with E_m = k_{2m}, O_m = k_{2m+1}, zero outside [0, N)
+__global__ void zmpc_ffa_taps(int N, const double* __restrict__ k, double* __restrict__ t) {
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= kffa_rows(N)) return;
+  const double e = (2 * m < N) ? k[2 * m] : 0.0;
+  const double o = (2 * m + 1 < N) ? k[2 * m + 1] : 0.0;
+  const double op = (m >= 1 && 2 * m - 1 < N) ? k[2 * m - 1] : 0.0;
+  t[4 * m + 0] = e;
+  t[4 * m + 1] = o;
+  t[4 * m + 2] = e + op;
+  t[4 * m + 3] = 0.0;
+}
+
 // 4. y = M⁻¹ e0 by two blocked triangular solves (64-row blocks), then k = Pu y, kx = k·Px.
 // One 1024-thread workgroup.  Per block: the off-block part of every row's dot product is a
 // wave reduction over coalesced row (forward) / column-block (backward) reads, the 64×64
@@ -515,6 +529,9 @@ hipError_t zmpc_launch_plan(zmpc_plan* P, hipStream_t s, hipEvent_t* ev) {
     return e;
   hipLaunchKernelGGL(zmpc_gain, dim3(1), dim3(1024), sizeof(double) * N, s, N, P->Kpad, P->L,
                      P->p, P->Px, P->k, P->kx);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(zmpc_ffa_taps, dim3((kffa_rows(N) + 63) / 64), dim3(64), 0, s, N, P->k,
+                     P->kffa);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if ((e = mark(4)) != hipSuccess) return e;
   hipLaunchKernelGGL(zmpc_scan_matrices, dim3(1), dim3(64), 0, s, P->T, P->T2_2, P->T3_6, P->kx,

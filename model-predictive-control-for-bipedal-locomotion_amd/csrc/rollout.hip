@@ -141,6 +141,7 @@ struct ZrLayout {
 
 struct RolloutGeom {
   int cw, passes, kc, lz, lzp, nf;
+  int kfm;  // fast-FIR steps (odd CW; axis_correlate_ffa), 0 otherwise
   int kcp;  // doubles of LDS for the staged gain row (kc rounded up to even)
 };
 
@@ -151,6 +152,13 @@ RolloutGeom rollout_geom(int N, int64_t n) {
   g.passes = (int)((nsteps + 64 * g.cw - 1) / (64 * g.cw));
   g.kc = (N + g.cw - 1) / g.cw * g.cw;           // k loop bound (k zero-padded)
   g.lz = g.passes * 64 * g.cw + g.kc + 1;         // z_ref samples staged (padded with last)
+  g.kfm = 0;
+  if (g.cw & 1) {
+    // the fast-FIR form (odd CW) reads up to sample 64·CW + 2·kfm + W of the walk
+    const int U = g.cw / 2 + 1, mm = (N + 2) / 2;
+    g.kfm = (mm + U - 1) / U * U;
+    g.lz = std::max(g.lz, g.passes * 64 * g.cw + 2 * g.kfm + 2 * U + 2);
+  }
   const int pad = (g.cw % 2 == 0) ? 1 : 0;
   g.lzp = g.lz + pad * (g.lz / g.cw) + 1;         // LDS doubles per axis
   // the z_ref area doubles as the history staging buffer: at least a third of a walk of rows
@@ -188,6 +196,8 @@ struct RolloutArgs {
   int fstride;
   const double2* fft_tw;  // plan twiddles e^{−2πi m/kFftPT} (FFT correlation, wide kernel)
   const double2* fft_g;   // plan gain spectrum DFT(g)/P for this launch's P
+  const double* kffa;     // plan fast-FIR taps [kffa_rows(N)][4] (axis_correlate_ffa)
+  int kfm;                // fast-FIR steps per walk, ⌈(N+1)/2⌉ rounded up to the unroll
 };
 
 // a 16-byte store with the non-temporal hint (streamed past the caches)
@@ -577,6 +587,61 @@ __device__ __forceinline__ void axis_correlate(const RolloutArgs& a, const doubl
   }
 }
 
+// The same correlation in two-parallel fast-FIR form (odd CW).  With g_j = z_ref[s + 1 + j]
+// (s = lane·CW), E_m = k_{2m}, O_m = k_{2m+1} and h_j = g_j + g_{j+1}, the half-length sums
+//   A(t) = Σ_m E_m g_{t+2m},  Bo(t) = Σ_m O_m g_{t+2m+1},  C(t) = Σ_m (E_m + O_{m−1}) h_{t+2m}
+// give f_t = A(t) + Bo(t) and f_{t+1} = C(t) − A(t) − Bo(t+2) (C(t) = A(t) + f_{t+1} + Bo(t+2)).
+// The lane's CW outputs are ⌊CW/2⌋ pairs (t = s + 2i) and one single (t = s + CW − 1, which
+// reuses the last pair's Bo(t+2)): ⌈CW/2⌉ A, ⌈CW/2⌉ Bo and ⌊CW/2⌋ C sums of ⌈(N+1)/2⌉ taps —
+// 11 × 76 FMAs + 76 additions (h) at CW = 7, N = 150, against 7 × 154 for the direct form.
+// A window of W = CW + 1 samples slides two per step (ring of W registers, renamed by the U-step
+// unroll), the h values a ring of U; one 16-byte pair of samples per step from LDS, the taps
+// (E_m, O_m, E_m + O_{m−1}) one wave-uniform row of the plan's table.
+template <int CW>
+__device__ __forceinline__ void axis_correlate_ffa(const RolloutArgs& a,
+                                                   const double* __restrict__ kt,
+                                                   const double* zr, int lane, double* f) {
+  static_assert(CW & 1, "the fast-FIR correlation takes odd chunk widths (no LDS padding)");
+  constexpr int NP = CW / 2, NA = NP + 1, NB = NP + 1, NC = NP, U = NP + 1, W = 2 * U;
+  const double* g = zr + lane * CW + 1;
+  double w[W], hr[U], A[NA], Bo[NB], C[NC > 0 ? NC : 1];
+#pragma unroll
+  for (int j = 0; j < W; ++j) w[j] = g[j];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    A[i] = 0.0;
+    Bo[i] = 0.0;
+  }
+#pragma unroll
+  for (int i = 0; i < NC; ++i) C[i] = 0.0;
+#pragma unroll
+  for (int i = 0; i + 1 < NC; ++i) hr[i] = w[2 * i] + w[2 * i + 1];  // h_{s+2i}
+  const int mloop = (a.dbg & 1) ? 0 : a.kfm;
+  const double* tr = kt;
+  for (int m0 = 0; m0 < mloop; m0 += U, tr += 4 * U) {
+#pragma unroll
+    for (int mm = 0; mm < U; ++mm) {
+      const double E = tr[4 * mm], O = tr[4 * mm + 1], EO = tr[4 * mm + 2];
+      const int b = 2 * mm;  // ring base (2m mod W: m0 is a multiple of U)
+      if (NC > 0) hr[(mm + NC - 1) % U] = w[(b + 2 * NC - 2) % W] + w[(b + 2 * NC - 1) % W];
+#pragma unroll
+      for (int i = 0; i < NA; ++i) A[i] = fma(E, w[(b + 2 * i) % W], A[i]);
+#pragma unroll
+      for (int i = 0; i < NB; ++i) Bo[i] = fma(O, w[(b + 2 * i + 1) % W], Bo[i]);
+#pragma unroll
+      for (int i = 0; i < NC; ++i) C[i] = fma(EO, hr[(mm + i) % U], C[i]);
+      w[b % W] = g[2 * (m0 + mm) + W];
+      w[(b + 1) % W] = g[2 * (m0 + mm) + W + 1];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    f[2 * i] = A[i] + Bo[i];
+    f[2 * i + 1] = (C[i] - A[i]) - Bo[i + 1];
+  }
+  f[CW - 1] = A[NP] + Bo[NP];
+}
+
 // Scan + replay + coalesced store of walk b's axis `axis` (f in registers); `stage` is the
 // walk's (dead) z_ref area, 2·lzp doubles, shared by both waves.
 template <int CW>
@@ -731,7 +796,8 @@ __global__ void __launch_bounds__(128, 8) zmpc_rollout_unc_axis_kernel(RolloutAr
 // PM (the persistent kernel): the walk's global loads and its history copy-out are issued at
 // raised wave priority, so a CU's co-resident walks get their memory traffic out ahead of the
 // others' correlation (config 2: 45.3 → 43.8 µs; the one-walk-per-workgroup grid is not helped).
-template <int CW, bool SHF = false, bool PM = false, int RND = 1, bool DPP = false>
+template <int CW, bool SHF = false, bool PM = false, int RND = 1, bool DPP = false,
+          bool FFA = false>
 __device__ __forceinline__ void split_walk(const RolloutArgs& a, int64_t b, double* smem,
                                            int* flag, const double* __restrict__ kg,
                                            const double* __restrict__ scanP,
@@ -777,7 +843,10 @@ __device__ __forceinline__ void split_walk(const RolloutArgs& a, int64_t b, doub
     }
     __syncthreads();
     // ---- 3. correlation (this wave's axis) -------------------------------------------------
-    axis_correlate<CW>(a, kg, axis ? zr1 : zr0, lane, f);  // k: wave-uniform scalar loads
+    if constexpr (FFA && (CW & 1))
+      axis_correlate_ffa<CW>(a, kg, axis ? zr1 : zr0, lane, f);  // kg = the fast-FIR taps
+    else
+      axis_correlate<CW>(a, kg, axis ? zr1 : zr0, lane, f);  // k: wave-uniform scalar loads
     __syncthreads();  // z_ref dead: the area becomes the history staging (n rows of 6)
   }
   // ---- 4. lane-chunk affine scan -----------------------------------------------------------
@@ -953,7 +1022,7 @@ __global__ void __launch_bounds__(128, 4)
 
 // The persistent split kernel with the DPP lane scan (scan_dpp): the default for config-2
 // shaped batches (variant 8; variant 15 = zmpc_rollout_unc_pers_kernel, the shuffle scan).
-template <int CW>
+template <int CW, bool FFA = true>
 __global__ void __launch_bounds__(128, 4)
     zmpc_rollout_unc_persd_kernel(RolloutArgs a, const double* __restrict__ kg,
                                   const double* __restrict__ scanP,
@@ -963,18 +1032,21 @@ __global__ void __launch_bounds__(128, 4)
   // (the tables through the argument struct: as __restrict__ arguments they go to SGPRs and
   // the DPP scan's per-lane powers push the kernel into spills)
   for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x) {
-    split_walk<CW, false, true, 1, true>(a, b, smem, flag, a.k, a.scanP, a.kx, a.hist);
+    split_walk<CW, false, true, 1, true, FFA>(a, b, smem, flag, (FFA && (CW & 1)) ? a.kffa : a.k,
+                                              a.scanP, a.kx, a.hist);
     __syncthreads();
   }
 }
 
 // One walk per workgroup with the DPP lane scan (variant 6 and large batches of variant 8;
 // variant 16 = zmpc_rollout_unc_split_kernel, the shuffle scan).
-template <int CW, bool SHF = false>
+template <int CW, bool SHF = false, bool FFA = true>
 __global__ void __launch_bounds__(128, 4) zmpc_rollout_unc_splitd_kernel(RolloutArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   __shared__ int flag[2];
-  split_walk<CW, SHF, false, 1, true>(a, blockIdx.x, smem, flag, a.k, a.scanP, a.kx, a.hist);
+  split_walk<CW, SHF, false, 1, true, FFA>(a, blockIdx.x, smem, flag,
+                                           (FFA && (CW & 1)) ? a.kffa : a.k, a.scanP, a.kx,
+                                           a.hist);
 }
 
 // Variant 11 (A/B): the persistent split kernel with the history copied out in two rounds, so
@@ -1857,16 +1929,26 @@ void launch_unc(const RolloutGeom& g, size_t lds, hipStream_t s, const RolloutAr
                          dim3(128), lds_i, s, a, a.k, a.scanP, a.kx, a.hist, region + 2);
     return;
   }
-  if (g.passes == 1 && (variant == 8 || variant == 6 || variant == 15 || variant == 16) &&
+  if (g.passes == 1 &&
+      (variant == 8 || variant == 6 || variant == 15 || variant == 16 || variant == 17 ||
+       variant == 18 || variant == 19) &&
       lds_split <= 64 * 1024) {
-    // 8 / 6: the lane scan on DPP moves (scan_dpp; round 3: one walk per workgroup 47.9 → 43.5
-    // µs at B = 4096, 94 → 87 µs at B = 8192, persistent 43.9 → 42.9 µs); 15 / 16: the same
-    // kernels with the round-2 shuffle scan (A/B)
-    const bool dpp = variant == 8 || variant == 6;
-    const void* pk = dpp ? reinterpret_cast<const void*>(zmpc_rollout_unc_persd_kernel<CW>)
-                         : reinterpret_cast<const void*>(zmpc_rollout_unc_pers_kernel<CW>);
+    // The lane scan on DPP moves (scan_dpp; round 3: one walk per workgroup 47.9 → 43.5 µs at
+    // B = 4096, 94 → 87 µs at B = 8192, persistent 43.9 → 42.9 µs) and, for odd CW, the fast-FIR
+    // correlation (axis_correlate_ffa).  8 (default): odd CW one walk per workgroup with the
+    // fast-FIR form (config 2, one box, three alternations: 41.6 µs vs 43.3 µs for the round-3
+    // default 17 and 44.7 µs for the persistent fast-FIR 19), even CW as 17; 6: one walk per
+    // workgroup; 17: persistent for B ≤ 3 × the resident grid, direct correlation; 18: one walk
+    // per workgroup, direct; 19: 17's grid with the fast-FIR form; 15 / 16: direct correlation
+    // and the round-2 shuffle scan (A/B)
+    const bool dpp = variant != 15 && variant != 16;
+    const bool ffa = (variant == 8 || variant == 6 || variant == 19) && (CW & 1);
+    const bool pers_v = (variant == 8 && !ffa) || variant == 15 || variant == 17 || variant == 19;
+    const void* pk = !dpp ? reinterpret_cast<const void*>(zmpc_rollout_unc_pers_kernel<CW>)
+                     : ffa ? reinterpret_cast<const void*>(zmpc_rollout_unc_persd_kernel<CW>)
+                           : reinterpret_cast<const void*>(zmpc_rollout_unc_persd_kernel<CW, false>);
     int per_cu = 0;
-    if ((variant == 8 || variant == 15) &&
+    if (pers_v &&
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pk, 128, lds_split) != hipSuccess)
       per_cu = 0;
     static const int per_cu_env = [] {
@@ -1878,15 +1960,21 @@ void launch_unc(const RolloutGeom& g, size_t lds, hipStream_t s, const RolloutAr
     // persistent only for a few walks per workgroup: config 2 (2 per workgroup) 45 µs vs
     // 49 µs; at 8 per workgroup (B = 16384) the one-walk grid is faster (156 vs 177 µs)
     if (per_cu > 0 && grid < a.B && a.B <= 3 * grid) {
-      if (dpp)
+      if (dpp && ffa)
         hipLaunchKernelGGL(zmpc_rollout_unc_persd_kernel<CW>, dim3((unsigned)grid), dim3(128),
                            lds_split, s, a, a.k, a.scanP, a.kx, a.hist);
+      else if (dpp)
+        hipLaunchKernelGGL((zmpc_rollout_unc_persd_kernel<CW, false>), dim3((unsigned)grid),
+                           dim3(128), lds_split, s, a, a.k, a.scanP, a.kx, a.hist);
       else
         hipLaunchKernelGGL(zmpc_rollout_unc_pers_kernel<CW>, dim3((unsigned)grid), dim3(128),
                            lds_split, s, a, a.k, a.scanP, a.kx, a.hist);
-    } else if (dpp) {
+    } else if (dpp && ffa) {
       hipLaunchKernelGGL(zmpc_rollout_unc_splitd_kernel<CW>, dim3((unsigned)a.B), dim3(128),
                          lds_split, s, a);
+    } else if (dpp) {
+      hipLaunchKernelGGL((zmpc_rollout_unc_splitd_kernel<CW, false, false>), dim3((unsigned)a.B),
+                         dim3(128), lds_split, s, a);
     } else {
       hipLaunchKernelGGL(zmpc_rollout_unc_split_kernel<CW>, dim3((unsigned)a.B), dim3(128),
                          lds_split, s, a);
@@ -1927,6 +2015,8 @@ hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, con
                 p->k, p->kx,  zmax,      zmin,  bstride,    x0,  kick,
                 kick_step,    hist, status, p->scanP, dbg, 0, kick_steps, nullptr, 0,
                 nullptr,      nullptr};
+  a.kffa = p->kffa;
+  a.kfm = g.kfm;
   WideGeom wg;
   static const bool no_wide = getenv("ZMPC_ROLLOUT_NO_WIDE") != nullptr;  // A/B: chunk kernel
   if (g.passes > 1 && (no_wide || !wide_geom(p->N, n, &wg))) {

@@ -43,6 +43,8 @@ struct zmpc_plan {
   double* L = nullptr;   // [N,N] lower Cholesky factor of M
   double* k = nullptr;   // [Kpad] gain row e0ᵀ M⁻¹ Puᵀ (zero-padded)
   double* kx = nullptr;  // [3]  k·Px
+  double* kffa = nullptr;  // [kffa_rows(N)][4] two-parallel fast-FIR taps of k (rollout.hip):
+                           // (E_m, O_m, E_m + O_{m−1}, 0), E_m = k_{2m}, O_m = k_{2m+1}, zero past N
   double* scanP = nullptr;  // [8][kScanLevels][9] (Ā^C)^(2^r) rollout scan propagators, then
                             // [8][33][9] (Ā^C)^k (kScanPowOff)
   double* X = nullptr;   // [N,N] L⁻¹ Puᵀ (strict plans)
@@ -64,6 +66,9 @@ struct zmpc_plan {
   // plan-build stage durations (zmpc_plan_timings), milliseconds
   float stage_ms[ZMPC_PLAN_STAGES] = {};
 };
+
+// rows of the fast-FIR tap table: m = 0..⌈(N+1)/2⌉−1, plus zero rows for an unrolled loop
+__host__ __device__ constexpr int kffa_rows(int N) { return (N + 2) / 2 + 8; }
 
 constexpr int kFftPT = 8192;    // largest transform (twiddle table size)
 constexpr int kFftPmin = 256;   // smallest transform with a gain spectrum

@@ -425,7 +425,7 @@ def test_rollout_kernel_variants_agree(tmp_path):
     inp = tmp_path / "in.npz"
     np.savez(inp, zmax=zmax, zmin=zmin, x0=x0, kick=kick, ks=n // 2, dt=dt)
     outs = []
-    for v in (8, 6, 15, 16, 1, 2, 9, 10, 11, 12):
+    for v in (8, 6, 15, 16, 17, 18, 19, 1, 2, 9, 10, 11, 12):
         out = tmp_path / f"h{v}.npy"
         env = dict(os.environ, ZMPC_ROLLOUT_VARIANT=str(v))
         subprocess.run([sys.executable, "-c", _VARIANT_CHILD, PKG, str(inp), str(out)],
