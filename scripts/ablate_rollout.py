@@ -30,11 +30,14 @@ print(json.dumps(dict(B=B, N=N, n=n, dbg=os.environ.get("ZMPC_DEBUG_ROLLOUT", "0
 
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 env0 = dict(os.environ, PKG=os.path.join(root, "model-predictive-control-for-bipedal-locomotion_amd"))
-VARIANTS = [dict(ZMPC_ROLLOUT_VARIANT=v) for v in ("8", "6", "1", "2")]
-for B, N, n in [(1024, 150, 420), (4096, 150, 420), (16384, 150, 420)]:
-  for var in VARIANTS:
-    for dbg in ((0, 1, 15) if B == 4096 else (0,)):
-        env = dict(env0, ZMPC_DEBUG_ROLLOUT=str(dbg), **var)
-        r = subprocess.run([sys.executable, "-c", CHILD, str(B), str(N), str(n)], env=env,
+# usage: ablate_rollout.py [variants=8,6,1,2] [dbg bits=0,1,15] [B=1024,4096,16384]
+VARIANTS = (sys.argv[1] if len(sys.argv) > 1 else "8,6,1,2").split(",")
+DBG = [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "0,1,15").split(",")]
+BS = [int(x) for x in (sys.argv[3] if len(sys.argv) > 3 else "1024,4096,16384").split(",")]
+for B in BS:
+  for v in VARIANTS:
+    for dbg in (DBG if B == 4096 else (0,)):
+        env = dict(env0, ZMPC_DEBUG_ROLLOUT=str(dbg), ZMPC_ROLLOUT_VARIANT=v)
+        r = subprocess.run([sys.executable, "-c", CHILD, str(B), "150", "420"], env=env,
                            capture_output=True, text=True, timeout=120)
         print(r.stdout.strip() or r.stderr[-500:], flush=True)
