@@ -340,6 +340,24 @@ __global__ void zmpc_scan_matrices(double T, double T2_2, double T3_6,
       for (int j = 0; j < 3; ++j)
         z[3 * i + j] = fma(x[3 * i + 0], y[0 + j], fma(x[3 * i + 1], y[3 + j], x[3 * i + 2] * y[6 + j]));
   };
+  {  // chunk-sum columns: V_p = Ā^p B, E_p = Ā^p e1
+    double V[3] = {Bv[0], Bv[1], Bv[2]}, E[3] = {0.0, 1.0, 0.0};
+    for (int p = 0; p < 8; ++p) {
+      for (int i = 0; i < 3; ++i) {
+        out[kScanGOff + p * 6 + i] = V[i];
+        out[kScanGOff + p * 6 + 3 + i] = E[i];
+      }
+      double v2[3], e2[3];
+      for (int i = 0; i < 3; ++i) {
+        v2[i] = fma(Ab[3 * i], V[0], fma(Ab[3 * i + 1], V[1], Ab[3 * i + 2] * V[2]));
+        e2[i] = fma(Ab[3 * i], E[0], fma(Ab[3 * i + 1], E[1], Ab[3 * i + 2] * E[2]));
+      }
+      for (int i = 0; i < 3; ++i) {
+        V[i] = v2[i];
+        E[i] = e2[i];
+      }
+    }
+  }
   double P[9];
   for (int q = 0; q < 9; ++q) P[q] = Ab[q];
   for (int C = 1; C <= 8; ++C) {

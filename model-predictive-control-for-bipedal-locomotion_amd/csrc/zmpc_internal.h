@@ -17,7 +17,10 @@ constexpr int kScanStride = kScanLevels * 9;
 // ... followed by the per-lane powers (Ā^C)^k, k = 0..32, [8][33][9] (the DPP scan's cross-row
 // steps, rollout.hip scan_dpp)
 constexpr int kScanPowOff = 8 * kScanStride;
-constexpr int kScanDoubles = kScanPowOff + 8 * 33 * 9;
+// ... and the chunk-sum columns Ā^p B, Ā^p e1 (p = 0..7), [8][6] (rollout.hip split_walk: a
+// lane's chunk end state Σ_q Ā^(C−1−q) B f_q, and the kick's Ā^(C−1−q) e1)
+constexpr int kScanGOff = kScanPowOff + 8 * 33 * 9;
+constexpr int kScanDoubles = kScanGOff + 8 * 6;
 
 // Longest strict horizon: the LQ kernel's per-wave slot flags ([N][64] bytes) must fit a CU's
 // LDS for one wave per workgroup (strict_lq.hip lq_variant_for).
