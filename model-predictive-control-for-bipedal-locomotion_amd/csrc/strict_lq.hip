@@ -89,7 +89,8 @@ struct LqArgs {
   double gipi, gam2, pig;  // γ/π, γ², πγ
   double tolnu;          // multiplier tolerance in the scaled objective (1e-13 / Q)
   int dbg;               // ZMPC_DEBUG_LQ (A/B diagnostics only): bit 0 = every wave reads the
-                         // staged bounds of group 0 (window traffic from cache; results wrong)
+                         // staged bounds of group 0 (window traffic from cache; results wrong),
+                         // bits 1 / 2 = x / y waves exit at once
 };
 
 struct Ric {  // value function V(x) = ½xᵀPx − sᵀx
@@ -614,6 +615,9 @@ __global__ void __launch_bounds__(64 * G, W)
     axis = (int)(gw & 1);
     b0 = (gw >> 1) * 64;
   }
+  // diagnostics: dbg bit 1 / bit 2 = the x / y waves of a rollout exit at once (the other
+  // axis then has its SIMDs alone; A/B timing only, results of that axis unwritten)
+  if (!a.window_mode && (((a.dbg & 2) && axis == 0) || ((a.dbg & 4) && axis == 1))) return;
   const int64_t b = b0 + lane;
   const bool valid = b < a.B;
   Lane L;
