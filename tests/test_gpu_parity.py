@@ -314,6 +314,25 @@ def test_walk_lengths(n):
     assert np.abs(hist.cpu().numpy() - ref).max() <= 1e-8
 
 
+@pytest.mark.parametrize("N", (1, 2, 3, 5, 150, 512))
+@pytest.mark.parametrize("n", (40, 130, 300, 420))
+def test_fast_fir_correlation_odd_chunk_widths(N, n):
+    """The fast-FIR correlation (rollout.hip axis_correlate_ffa) runs for odd chunk widths:
+    n = 40 / 130 / 300 / 420 give CW = 1 / 3 / 5 / 7; horizons from one tap (no pair sums) to
+    512 (tap table and window padding past the unrolled steps).  Every walk vs the oracle."""
+    rng = np.random.default_rng(10 * N + n)
+    dt = 0.01
+    ctr = np.cumsum(rng.normal(0, 0.01, (3, n, 2)), 1)
+    zmax, zmin = ctr + 0.05, ctr - 0.05
+    x0 = rng.normal(0, 0.01, (3, 2, 3))
+    kick = np.array([0.1, 0.0, -0.2])
+    p = plan(N, dt=dt)
+    hist, st = p.rollout(zmax, zmin, x0, kick=kick, kick_step=n // 2)
+    assert int(st.abs().max()) == 0
+    ref = O.rollout_gain(zmax, zmin, x0, N, dt, H, G, Q, R, kick, n // 2)
+    assert np.abs(hist.cpu().numpy() - ref).max() <= 1e-8
+
+
 @pytest.mark.parametrize("N,n", ((512, 3649), (512, 3650), (512, 5000), (150, 6001)))
 def test_long_walks_any_length(N, n):
     """Walks longer than one LDS-resident pass (n > 3649 at N = 512 was rejected before the
