@@ -319,7 +319,9 @@ def test_walk_lengths(n):
 def test_fast_fir_correlation_odd_chunk_widths(N, n):
     """The fast-FIR correlation (rollout.hip axis_correlate_ffa) runs for odd chunk widths:
     n = 40 / 130 / 300 / 420 give CW = 1 / 3 / 5 / 7; horizons from one tap (no pair sums) to
-    512 (tap table and window padding past the unrolled steps).  Every walk vs the oracle."""
+    512 (tap table and window padding past the unrolled steps).  Every walk vs the oracle;
+    horizons below ≈10 samples do not stabilise the walk (states reach 1e6 by n = 420), so the
+    bound is relative to the largest state."""
     rng = np.random.default_rng(10 * N + n)
     dt = 0.01
     ctr = np.cumsum(rng.normal(0, 0.01, (3, n, 2)), 1)
@@ -330,7 +332,7 @@ def test_fast_fir_correlation_odd_chunk_widths(N, n):
     hist, st = p.rollout(zmax, zmin, x0, kick=kick, kick_step=n // 2)
     assert int(st.abs().max()) == 0
     ref = O.rollout_gain(zmax, zmin, x0, N, dt, H, G, Q, R, kick, n // 2)
-    assert np.abs(hist.cpu().numpy() - ref).max() <= 1e-8
+    assert np.abs(hist.cpu().numpy() - ref).max() <= 1e-8 * max(1.0, np.abs(ref).max())
 
 
 @pytest.mark.parametrize("N,n", ((512, 3649), (512, 3650), (512, 5000), (150, 6001)))
