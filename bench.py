@@ -195,6 +195,7 @@ def herdt_bench(args, rank, world, dev):
                      "kernel": "zmpc_herdt_kernel", "kernel_ms": kern_ms,
                      "alg_flops_per_launch": flops,
                      "passes_per_solve": passes_per_solve,
+                     "max_passes_per_solve": cnt["herdt_max_passes_per_solve"],
                      "wave_passes_per_launch": cnt["herdt_wave_passes"] / args.steps,
                      "engine": "FP64 VALU, one (walk, axis) per lane; FLOPs = minimal per-row "
                                "work x the executed active-set passes (kernel counters)"},
@@ -889,6 +890,7 @@ def main():
                     "engine": "FP64 VALU (one instance per lane; no MFMA-shaped work)",
                     "strict_alg_flops_per_launch": sflops,
                     "passes_per_solve": work["instance_passes"] / per / (B * (n - 1) * 2),
+                    "max_passes_per_solve": work["max_passes_per_solve"],
                     "lane_efficiency": work["instance_passes"] / max(1, 64 * work["wave_passes"]),
                     "working_set_slot_frac": ws / max(1, slots)}
         roof.update({

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define ZMPC_ABI_VERSION 5
+#define ZMPC_ABI_VERSION 6
 
 /* return codes */
 #define ZMPC_OK 0
@@ -91,10 +91,13 @@ int zmpc_plan_export(const zmpc_plan* plan, int32_t what, double* dst_host, int6
  * Herdt joint footstep QP (zmpc_herdt_rollout / zmpc_herdt_step, any plan; since ABI 4):
  *   [4] wave passes, [5] instance passes (one instance = one walk axis),
  *   [6] sum over instance passes of the window's footstep count m, [7] the same of m^2
+ * Maxima (since ABI 6): [8] the most active-set passes any one strict solve took,
+ *   [9] the same for the Herdt solver (passes of the solve's lane pair)
  * count = number of uint64 dst can hold (at most ZMPC_NCOUNTERS are written); reset != 0
- * zeroes the counters after the copy.  Since ABI 3 ([0..3]); [4..7] since ABI 4.
+ * zeroes the counters after the copy.  Since ABI 3 ([0..3]); [4..7] since ABI 4; [8..9]
+ * since ABI 6.
  */
-#define ZMPC_NCOUNTERS 8
+#define ZMPC_NCOUNTERS 10
 int zmpc_plan_counters(const zmpc_plan* plan, uint64_t* dst_host, int32_t count, int32_t reset);
 
 /*

@@ -473,6 +473,7 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
   for (int k = 0; k < N; ++k) wset[k * 64 + lane] = 0;
   int fq = 0;
   unsigned long long n_wave_pass = 0, n_pass = 0, n_m = 0, n_m2 = 0;
+  unsigned itmax = 0;  // most passes of one solve (counter [9])
   unsigned long long pr_b = 0, pr_f = 0, pr_w = 0, pr_t0 = a.prof ? clock64() : 0;
   unsigned long long pr_kw = 0, pr_ns = 0;
   const int64_t nsteps = a.window_mode ? 1 : a.n - 1;
@@ -543,7 +544,7 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
     double u0 = 0.0, f0 = 0.0;
     double fsol[MM > 0 ? MM : 1];
     int it = 0;
-    bool again = true;
+    bool again = true;  // (itmax: the most passes of one solve, counter [9])
     while (again) {
       const unsigned long long tp0 = a.prof ? clock64() : 0;
       // ---- sweep 1: backward Riccati over ξ = [x; f] for V_0(x, f), then the footsteps -----
@@ -821,6 +822,7 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
       // the pair runs its passes together (the polytope solve reads both lanes)
       again = __any(changed && valid);
     }
+    if (valid) itmax = max(itmax, (unsigned)it);
     // ---- advance (reference form x⁺ = A x + B u0, zmp_controller.py:809-810) ----------------
     double xn[3];
     xn[0] = x[0] + T * x[1] + T2 * x[2] + T3 * u0;
@@ -886,12 +888,14 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
       n_pass += __shfl_xor(n_pass, o);
       n_m += __shfl_xor(n_m, o);
       n_m2 += __shfl_xor(n_m2, o);
+      itmax = max(itmax, (unsigned)__shfl_xor((int)itmax, o));
     }
     if (lane == 0) {
       atomicAdd(a.cnt + 4, n_wave_pass);
       atomicAdd(a.cnt + 5, n_pass);
       atomicAdd(a.cnt + 6, n_m);
       atomicAdd(a.cnt + 7, n_m2);
+      atomicMax(a.cnt + 9, (unsigned long long)itmax);
     }
   }
 }

@@ -658,6 +658,7 @@ __global__ void __launch_bounds__(64 * G, W)
   int64_t i = 0;
   bool active = valid && a.nsteps > 0;
   int it = 0;
+  unsigned itmax = 0;  // most passes of one of this lane's solves (counter [8])
   int klast = -1;  // last active slot of this lane's working set (−1: none)
   while (__any(active)) {
     ++n_wave_pass;
@@ -809,6 +810,7 @@ __global__ void __launch_bounds__(64 * G, W)
         changed = false;
       }
       if (!changed) {
+        itmax = max(itmax, (unsigned)it);
         // converged: advance in the reference form x⁺ = A x + B u0 (zmp_controller.py:199)
         u0 = u0 / a.Tcu;  // v0 = T³ u0
         double xn[3];
@@ -864,12 +866,14 @@ __global__ void __launch_bounds__(64 * G, W)
     for (int o = 32; o > 0; o >>= 1) {
       n_lane_pass += __shfl_xor(n_lane_pass, o);
       n_ws_slots += __shfl_xor(n_ws_slots, o);
+      itmax = max(itmax, (unsigned)__shfl_xor((int)itmax, o));
     }
     if (lane == 0) {
       atomicAdd(a.cnt + 0, n_wave_pass);
       atomicAdd(a.cnt + 1, n_lane_pass);
       atomicAdd(a.cnt + 2, n_ws_slots);
       if (gw == 0) atomicAdd(a.cnt + 3, 1ull);
+      atomicMax(a.cnt + 8, (unsigned long long)itmax);
     }
   }
 }

@@ -12,8 +12,8 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ZMPC_LIB", os.path.join(_HERE, "libzmpc.so"))
 
-ABI_VERSION = 5  # include/zmpc.h ZMPC_ABI_VERSION this binding is written for
-NCOUNTERS = 8    # include/zmpc.h ZMPC_NCOUNTERS
+ABI_VERSION = 6  # include/zmpc.h ZMPC_ABI_VERSION this binding is written for
+NCOUNTERS = 10   # include/zmpc.h ZMPC_NCOUNTERS
 PLAN_STAGES = 12  # include/zmpc.h ZMPC_PLAN_STAGES
 PLAN_STAGE_NAMES = ("prediction", "gram_PuTPu", "cholesky", "gain", "scan", "fft_tables",
                     "strict_X", "strict_gram_G", "strict_Pu_inverse", "strict_gram_Hz",

@@ -100,7 +100,8 @@ class Plan:
         return {"wave_passes": int(buf[0]), "instance_passes": int(buf[1]),
                 "working_set_slots": int(buf[2]), "launches": int(buf[3]),
                 "herdt_wave_passes": int(buf[4]), "herdt_instance_passes": int(buf[5]),
-                "herdt_footsteps": int(buf[6]), "herdt_footsteps_sq": int(buf[7])}
+                "herdt_footsteps": int(buf[6]), "herdt_footsteps_sq": int(buf[7]),
+                "max_passes_per_solve": int(buf[8]), "herdt_max_passes_per_solve": int(buf[9])}
 
     def timings(self) -> dict:
         """Plan-build stage durations in ms (zmpc_plan_timings; HIP events on the creation

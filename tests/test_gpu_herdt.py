@@ -121,6 +121,8 @@ def test_herdt_work_counters():
     assert k["herdt_instance_passes"] >= 2 * B * (n - 1)
     assert k["herdt_wave_passes"] * 64 >= k["herdt_instance_passes"]
     assert k["herdt_footsteps_sq"] >= k["herdt_footsteps"] >= 0
+    # [9]: the most passes of one solve — at least the mean, at most the cap
+    assert k["herdt_instance_passes"] / (2 * B * (n - 1)) <= k["herdt_max_passes_per_solve"] <= 64
 
 
 def _ragged_schedules(B, n=90):

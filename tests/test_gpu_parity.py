@@ -583,6 +583,8 @@ def test_strict_work_counters():
     assert solves <= c["instance_passes"] <= 3 * solves
     assert 0 < c["working_set_slots"] < c["instance_passes"] * 150
     assert c["wave_passes"] * 64 >= c["instance_passes"]
+    # [8]: the most passes of one solve — at least the mean, at most the cap
+    assert c["instance_passes"] / solves <= c["max_passes_per_solve"] <= 64
     assert p.counters()["launches"] == 0
 
 

@@ -92,7 +92,7 @@ def test_library_loads_and_exports_every_symbol():
     exported = set(re.findall(r" T (zmpc_\w+)", out))
     assert set(_header_symbols()) <= exported
     lib = _native.load()
-    assert lib.zmpc_abi_version() == _native.ABI_VERSION == 5
+    assert lib.zmpc_abi_version() == _native.ABI_VERSION == 6
     assert lib.zmpc_last_error() == b""
 
 
