@@ -1035,8 +1035,10 @@ void fill_consts(const zmpc_plan* p, LqArgs& a) {
   a.pig = a.pi * a.gam;
   a.tolnu = 1e-13 / p->Q;
   static const int drift = [] {
-    const char* e = getenv("ZMPC_STRICT_LQ_DRIFT");  // A/B only
-    return e ? atoi(e) : 2;
+    // A/B only; round 3 (profiles/r3u/): 0 → 104.5 ms, 1 → 94.8, 2 → 92.5, 3 → 91.1,
+    // 4 → 90.9, 8 → 92.7 at config 3 (config 4: 2 → 143.1, 4 → 140.8 ms)
+    const char* e = getenv("ZMPC_STRICT_LQ_DRIFT");
+    return e ? atoi(e) : 4;
   }();
   a.drift = drift;
   a.cnt = p->lqcnt;
