@@ -1,15 +1,18 @@
 #!/bin/bash
-# Round profile: bench (default = BASELINE config 2), rocprofv3 kernel stats, HBM PMC passes
-# (FETCH_SIZE / WRITE_SIZE in their own runs, kernel-trace only), final bench with traffic.
-# Usage: bash scripts/gpu_profile_round.sh <tag>      outputs under gpurun_out/<tag>/
+# Round profile: bench, rocprofv3 kernel stats, HBM PMC passes (FETCH_SIZE / WRITE_SIZE in their
+# own runs, kernel-trace only), then the bench again with the traffic it now reads.
+# Usage: bash scripts/gpu_profile_round.sh <tag> [workload kernel-substring bench-args...]
+#   default: config2_n150_b4096 zmpc_rollout_unc "--steps 20 --warmup 3"
+# outputs under gpurun_out/<tag>/
 set -u
 TAG=${1:-round}
+WL=${2:-config2_n150_b4096}
+K=${3:-zmpc_rollout_unc}
+shift 3 2>/dev/null || shift $#
+ARGS="${*:---steps 20 --warmup 3} --no-cpu-baseline"
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-WL=config2_n150_b4096
-K=zmpc_rollout_unc
-ARGS="--steps 20 --warmup 3 --no-cpu-baseline"
 step() { echo "== $1 rc=$2"; if [ "$2" -ne 0 ]; then exit "$2"; fi; }
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o bench -- \
     python3 bench.py $ARGS > "$OUT/stats_bench.json" 2> "$OUT/stats.err"
@@ -23,6 +26,6 @@ step write $?
 python3 profiles/collect_pmc.py "$OUT" "$WL" "$K" > "$OUT/pmc.json"
 step collect $?
 cp profiles/pmc_$WL.json "$OUT/"
-timeout -k 10 600 python3 bench.py > "$OUT/bench.json" 2> "$OUT/bench.err"
+timeout -k 10 600 python3 bench.py $ARGS > "$OUT/bench.json" 2> "$OUT/bench.err"
 step bench $?
 cat "$OUT/bench.json"
