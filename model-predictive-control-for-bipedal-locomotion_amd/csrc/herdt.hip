@@ -475,7 +475,7 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
   unsigned long long n_wave_pass = 0, n_pass = 0, n_m = 0, n_m2 = 0;
   unsigned itmax = 0;  // most passes of one solve (counter [9])
   unsigned long long pr_b = 0, pr_f = 0, pr_w = 0, pr_t0 = a.prof ? clock64() : 0;
-  unsigned long long pr_kw = 0, pr_ns = 0;
+  unsigned long long pr_kw = 0, pr_ns = 0, pr_own = 0;
   const int64_t nsteps = a.window_mode ? 1 : a.n - 1;
   const int64_t kstep = (!a.window_mode && axis == 1 && a.kick) ? a.kick_step : -1;
   const double kv = (kstep >= 0 && valid) ? a.kick[wc] : 0.0;
@@ -543,7 +543,8 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
 
     double u0 = 0.0, f0 = 0.0;
     double fsol[MM > 0 ? MM : 1];
-    int it = 0;
+    int it = 0, own = 0;  // own: the passes this lane pair needed (diagnostics, ZMPC_HERDT_PROF)
+    bool pair_done = false;
     bool again = true;  // (itmax: the most passes of one solve, counter [9])
     while (again) {
       const unsigned long long tp0 = a.prof ? clock64() : 0;
@@ -810,6 +811,13 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
       }
       ++it;
       ++n_wave_pass;
+      if (a.prof) {
+        const bool pch = changed || (__shfl_xor(changed ? 1 : 0, 1, 64) != 0);
+        if (!pair_done) {
+          ++own;
+          pair_done = !pch;
+        }
+      }
       if (valid) {
         ++n_pass;
         n_m += (unsigned)m;
@@ -823,6 +831,7 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
       again = __any(changed && valid);
     }
     if (valid) itmax = max(itmax, (unsigned)it);
+    if (valid) pr_own += (unsigned long long)own;
     // ---- advance (reference form x⁺ = A x + B u0, zmp_controller.py:809-810) ----------------
     double xn[3];
     xn[0] = x[0] + T * x[1] + T2 * x[2] + T3 * u0;
@@ -872,7 +881,10 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
     if (axis == 0) a.status[wc] = fq | other;
   }
   if (a.prof) {
-    for (int o = 32; o > 0; o >>= 1) pr_ns += __shfl_xor(pr_ns, o);
+    for (int o = 32; o > 0; o >>= 1) {
+      pr_ns += __shfl_xor(pr_ns, o);
+      pr_own += __shfl_xor(pr_own, o);
+    }
     if (lane == 0) {
       atomicAdd(a.prof + 0, pr_b);
       atomicAdd(a.prof + 1, pr_f);
@@ -881,6 +893,7 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
       atomicAdd(a.prof + 4, pr_kw);
       atomicAdd(a.prof + 5, pr_ns);
       atomicAdd(a.prof + 6, n_wave_pass);
+      atomicAdd(a.prof + 7, pr_own);
     }
   }
   if (a.cnt) {
@@ -1001,9 +1014,10 @@ hipError_t zmpc_launch_herdt(const zmpc_plan* p, const zmpc_herdt_params* prm, i
     const double t = (double)(h[3] ? h[3] : 1), wp = (double)(h[6] ? h[6] : 1);
     fprintf(stderr,
             "herdt prof: backward %.3f footsteps %.3f forward %.3f (of %llu clocks/wave); "
-            "rows to the wave's last pinned row %.1f, pinned rows per lane %.2f (per pass)\n",
+            "rows to the wave's last pinned row %.1f, pinned rows per lane %.2f (per pass); "
+            "lane-pair passes needed %llu vs wave passes x 64 %llu\n",
             h[0] / t, h[1] / t, h[2] / t, h[3] / (unsigned long long)blocks, h[4] / wp,
-            h[5] / (wp * 64));
+            h[5] / (wp * 64), h[7], h[6] * 64);
   }
   return e != hipSuccess ? e : ef;
 }
