@@ -74,6 +74,7 @@ struct LqArgs {
   const double* kick;    // [B] or null
   int64_t kick_step;
   const int64_t* kick_steps;
+  const int32_t* perm;   // walk of lane position b0 + lane (order.hip), or null (identity)
   double* out;           // rollout hist [B,n,2,3], step x_next [B,3]
   int32_t* status;
   double* ck;            // checkpoints [waves][NS][9][64]
@@ -114,6 +115,7 @@ constexpr double kH = 0.5, kS6 = 1.0 / 6.0;
 
 // One backward Riccati step in scaled coordinates (see header and LqArgs), per-lane slot flag
 // f.  Inputs: V_{k+1} in v, bounds.  Outputs the step's feedback v_k = −K ξ_k − kff.
+template <bool LEAN>
 __device__ __forceinline__ void ric_step(const LqArgs& a, Ric& v, double hi, double lo, int f,
                                          double& K0, double& K1, double& K2, double& kf) {
   // P B̂, B̂ᵀs, B̂ᵀPB̂
@@ -142,24 +144,55 @@ __device__ __forceinline__ void ric_step(const LqArgs& a, Ric& v, double hi, dou
   double iq = __builtin_amdgcn_rcp(Quu);
   iq = fma(iq, fma(-Quu, iq, 1.0), iq);
   iq = fma(iq, fma(-Quu, iq, 1.0), iq);
-  const double t = (f == 1) ? hi : lo;
-  K0 = act ? a.ipi : ux0 * iq;
-  K1 = act ? a.ipi : ux1 * iq;
-  K2 = act ? a.gipi : ux2 * iq;
-  kf = act ? -t * a.ipi : qu * iq;
-  const double D0 = act ? fma(Quu, K0, -ux0) : 0.0;
-  const double D1 = act ? fma(Quu, K1, -ux1) : 0.0;
-  const double D2 = act ? fma(Quu, K2, -ux2) : 0.0;
-  // P = ĉĉᵀ + ÂᵀPÂ − Qux Kᵀ + K Dᵀ   (ĉĉᵀ = [[1,1,γ],[1,1,γ],[γ,γ,γ²]])
-  const double P00 = fma(K0, D0, fma(-ux0, K0, 1.0 + v.p00));
-  const double P01 = fma(K0, D1, fma(-ux0, K1, 1.0 + m01));
-  const double P02 = fma(K0, D2, fma(-ux0, K2, a.gam + m02));
-  const double P11 = fma(K1, D1, fma(-ux1, K1, 1.0 + S11));
-  const double P12 = fma(K1, D2, fma(-ux1, K2, a.gam + S12));
-  const double P22 = fma(K2, D2, fma(-ux2, K2, a.gam2 + S22));
-  v.s0 = fma(-kf, D0, fma(K0, qu, nqx0));
-  v.s1 = fma(-kf, D1, fma(K1, qu, nqx1));
-  v.s2 = fma(-kf, D2, fma(K2, qu, nqx2));
+  double P00, P01, P02, P11, P12, P22;
+  if constexpr (LEAN) {
+    // Few per-lane selects (each a pair of v_cndmask_b32): the free part (iqa) and the active
+    // part (ka, kfa, zero at free slots) of the law, K = Qux·iqa + ka and kff = qu·iqa + kfa —
+    // exactly ux·iq / qu·iq at a free slot and ĉ/π / −t/π at an active one.  D = Quu K − Qux is
+    // formed unconditionally (rounding noise at free slots) and enters only through ka and kfa,
+    // which vanish there: the same values as the per-field selects, up to the sign of a zero.
+    const double iqa = act ? 0.0 : iq;
+    const double ka01 = act ? a.ipi : 0.0;
+    const double ka2 = act ? a.gipi : 0.0;
+    const double tz = (f == 1) ? hi : ((f == 2) ? lo : 0.0);
+    const double kfa = -tz * a.ipi;
+    K0 = fma(ux0, iqa, ka01);
+    K1 = fma(ux1, iqa, ka01);
+    K2 = fma(ux2, iqa, ka2);
+    kf = fma(qu, iqa, kfa);
+    const double D0 = fma(Quu, K0, -ux0);
+    const double D1 = fma(Quu, K1, -ux1);
+    const double D2 = fma(Quu, K2, -ux2);
+    // P = ĉĉᵀ + ÂᵀPÂ − Qux Kᵀ + K Dᵀ   (ĉĉᵀ = [[1,1,γ],[1,1,γ],[γ,γ,γ²]])
+    P00 = fma(ka01, D0, fma(-ux0, K0, 1.0 + v.p00));
+    P01 = fma(ka01, D1, fma(-ux0, K1, 1.0 + m01));
+    P02 = fma(ka01, D2, fma(-ux0, K2, a.gam + m02));
+    P11 = fma(ka01, D1, fma(-ux1, K1, 1.0 + S11));
+    P12 = fma(ka01, D2, fma(-ux1, K2, a.gam + S12));
+    P22 = fma(ka2, D2, fma(-ux2, K2, a.gam2 + S22));
+    v.s0 = fma(-kfa, D0, fma(K0, qu, nqx0));
+    v.s1 = fma(-kfa, D1, fma(K1, qu, nqx1));
+    v.s2 = fma(-kfa, D2, fma(K2, qu, nqx2));
+  } else {
+    // per-field selects (sweep B: the lean form above needs more registers there)
+    const double t = (f == 1) ? hi : lo;
+    K0 = act ? a.ipi : ux0 * iq;
+    K1 = act ? a.ipi : ux1 * iq;
+    K2 = act ? a.gipi : ux2 * iq;
+    kf = act ? -t * a.ipi : qu * iq;
+    const double D0 = act ? fma(Quu, K0, -ux0) : 0.0;
+    const double D1 = act ? fma(Quu, K1, -ux1) : 0.0;
+    const double D2 = act ? fma(Quu, K2, -ux2) : 0.0;
+    P00 = fma(K0, D0, fma(-ux0, K0, 1.0 + v.p00));
+    P01 = fma(K0, D1, fma(-ux0, K1, 1.0 + m01));
+    P02 = fma(K0, D2, fma(-ux0, K2, a.gam + m02));
+    P11 = fma(K1, D1, fma(-ux1, K1, 1.0 + S11));
+    P12 = fma(K1, D2, fma(-ux1, K2, a.gam + S12));
+    P22 = fma(K2, D2, fma(-ux2, K2, a.gam2 + S22));
+    v.s0 = fma(-kf, D0, fma(K0, qu, nqx0));
+    v.s1 = fma(-kf, D1, fma(K1, qu, nqx1));
+    v.s2 = fma(-kf, D2, fma(K2, qu, nqx2));
+  }
   v.p00 = P00;
   v.p01 = P01;
   v.p02 = P02;
@@ -344,7 +377,7 @@ __device__ __forceinline__ void seg_riccati(const LqArgs& a, int j, Ric& v, cons
         double iq;
         ric_free(a, v, (in.hi[q] + in.lo[q]) / 2, K0, K1, K2, kf, iq);
       } else {
-        ric_step(a, v, in.hi[q], in.lo[q], in.f[q], K0, K1, K2, kf);
+        ric_step<!KEEP>(a, v, in.hi[q], in.lo[q], in.f[q], K0, K1, K2, kf);
       }
       if (KEEP) {
         g.K0[q] = K0;
@@ -618,8 +651,10 @@ __global__ void __launch_bounds__(64 * G, W)
   // diagnostics: dbg bit 1 / bit 2 = the x / y waves of a rollout exit at once (the other
   // axis then has its SIMDs alone; A/B timing only, results of that axis unwritten)
   if (!a.window_mode && (((a.dbg & 2) && axis == 0) || ((a.dbg & 4) && axis == 1))) return;
-  const int64_t b = b0 + lane;
-  const bool valid = b < a.B;
+  // lane position b0 + lane runs walk b (the kick order of order.hip, or the identity); the
+  // staged bounds follow the positions, everything per walk (x0, kick, history, status) b
+  const bool valid = b0 + lane < a.B;
+  const int64_t b = (valid && a.perm) ? (int64_t)a.perm[b0 + lane] : b0 + lane;
   Lane L;
   L.lane = lane;
   {
@@ -912,6 +947,7 @@ struct StageArgs {
   int64_t sb, st, sa, nsrc;
   int64_t B, G, rows;
   int naxes;
+  const int32_t* perm;  // destination position p takes walk perm[p] (null: p)
   double2* dst;
 };
 
@@ -923,11 +959,12 @@ __global__ void __launch_bounds__(256) zmpc_bounds_stage_kernel(StageArgs s) {
   for (int idx = threadIdx.x; idx < 64 * per_walk; idx += 256) {
     const int w = idx / per_walk, rem = idx - w * per_walk;
     const int tt = rem / s.naxes, ax = rem - tt * s.naxes;
-    const int64_t b = b0 + w;
+    int64_t b = b0 + w;
     int64_t t = t0 + tt;
     if (t > s.nsrc - 1) t = s.nsrc - 1;  // window padding (zmp_controller.py:81-88)
     double2 v = make_double2(0.0, 0.0);
     if (b < s.B) {
+      if (s.perm) b = s.perm[b];
       const int64_t e = b * s.sb + t * s.st + ax * s.sa;
       v = make_double2(s.hi[e], s.lo[e]);
     }
@@ -944,8 +981,9 @@ __global__ void __launch_bounds__(256) zmpc_bounds_stage_kernel(StageArgs s) {
 }
 
 hipError_t stage(const double* hi, const double* lo, int64_t sb, int64_t st, int64_t sa,
-                 int64_t nsrc, int64_t B, int64_t rows, int naxes, double2* dst, hipStream_t s) {
-  StageArgs g{hi, lo, sb, st, sa, nsrc, B, (B + 63) / 64, rows, naxes, dst};
+                 int64_t nsrc, int64_t B, int64_t rows, int naxes, double2* dst, hipStream_t s,
+                 const int32_t* perm = nullptr) {
+  StageArgs g{hi, lo, sb, st, sa, nsrc, B, (B + 63) / 64, rows, naxes, perm, dst};
   const dim3 grid((unsigned)((rows + 15) / 16), (unsigned)g.G);
   hipLaunchKernelGGL(zmpc_bounds_stage_kernel, grid, dim3(256), 0, s, g);
   return hipGetLastError();
@@ -1127,14 +1165,33 @@ hipError_t zmpc_launch_rollout_strict_lq(const zmpc_plan* p, int64_t B, int64_t 
   const int64_t G = lq_variant_for(p->N).G;  // checkpoints for every wave of the launched blocks
   const size_t ck_doubles = (size_t)((waves + G - 1) / G * G) * a.NS * 10 * 64;  // ≥ either layout
   const size_t st_doubles = (size_t)2 * a.groups * a.rows * 64 * 2;  // 2 axes, (hi, lo)
+  // kick order (order.hip): walks with per-walk kicks sorted by (kick step, kick) onto lanes,
+  // when there is more than one wave of them (ZMPC_STRICT_ORDER=0 keeps the input order; A/B)
+  static const bool order_on = [] {
+    const char* e = getenv("ZMPC_STRICT_ORDER");
+    return !(e && atoi(e) == 0);
+  }();
+  const bool ordered = order_on && kick != nullptr && B > 64;
+  const size_t perm_doubles = ordered ? ((size_t)B * 4 + 7) / 8 : 0;
+  const size_t ord_doubles = ordered ? (zmpc_kick_order_bytes(B) + 7) / 8 : 0;
   double* ws = nullptr;
-  if (hipMallocAsync((void**)&ws, (ck_doubles + st_doubles) * sizeof(double), s) != hipSuccess) {
+  if (hipMallocAsync((void**)&ws,
+                     (ck_doubles + st_doubles + perm_doubles + ord_doubles) * sizeof(double),
+                     s) != hipSuccess) {
     (void)hipGetLastError();
     return hipErrorOutOfMemory;  // ZMPC_ENOMEM at the C-ABI
   }
   a.ck = ws;
   double2* hl = reinterpret_cast<double2*>(ws + ck_doubles);
-  e = stage(zmax, zmin, bstride, 2, 1, n, Bst, a.rows, 2, hl, s);
+  a.perm = nullptr;
+  if (ordered) {
+    int32_t* perm = reinterpret_cast<int32_t*>(ws + ck_doubles + st_doubles);
+    e = zmpc_kick_order(kick, kick_steps, kick_step, B, perm,
+                        ws + ck_doubles + st_doubles + perm_doubles, s);
+    a.perm = perm;
+  }
+  if (e == hipSuccess)
+    e = stage(zmax, zmin, bstride, 2, 1, n, Bst, a.rows, 2, hl, s, a.shared ? nullptr : a.perm);
   a.hl = hl;
   if (e == hipSuccess) e = launch_lq(p, a, waves, s);
   hipError_t ef = hipFreeAsync(ws, s);

@@ -126,6 +126,13 @@ hipError_t zmpc_strict_lq_set_attrs();
 size_t zmpc_strict_lq_table_doubles(int N);
 hipError_t zmpc_strict_lq_build_table(zmpc_plan* p, hipStream_t s);
 
+// walk order for the lane-per-instance kernels (order.hip): perm[B] = the walks sorted by
+// (kick step, kick), so that a wave's lanes take similar disturbances; ws of
+// zmpc_kick_order_bytes(B) bytes (device, stream-ordered)
+size_t zmpc_kick_order_bytes(int64_t B);
+hipError_t zmpc_kick_order(const double* kick, const int64_t* kick_steps, int64_t kick_step,
+                           int64_t B, int32_t* perm, void* ws, hipStream_t s);
+
 // Herdt joint footstep QP (herdt.hip); support states as cop_generator.State
 constexpr int ZMPC_STANDING = 0, ZMPC_DOUBLE_SUPPORT = 1, ZMPC_SINGLE_SUPPORT = 2;
 hipError_t zmpc_launch_herdt(const zmpc_plan* p, const zmpc_herdt_params* prm, int64_t B,

@@ -567,6 +567,58 @@ def test_strict_translation_invariance_full_batch():
     assert np.abs(d[..., 0] - 0.0625).max() <= 1e-7
 
 
+_ORDER_CHILD = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, sys.argv[1])
+from mpc_bipedal.solver import Plan
+d = np.load(sys.argv[2])
+p = Plan(0, 150, float(d["dt"]), 0.75, 9.81, 1.0, 1e-6, True)
+h, st = p.rollout(d["zmax"], d["zmin"], d["x0"], kick=d["kick"], kick_step=d["ks"])
+c = p.counters()
+np.savez(sys.argv[3], h=h.cpu().numpy(), st=st.cpu().numpy(), wp=c["wave_passes"],
+         ip=c["instance_passes"])
+"""
+
+
+@pytest.mark.parametrize("shared", (False, True))
+def test_strict_kick_order_same_results(tmp_path, shared):
+    """order.hip: walks with per-walk kicks are mapped to lanes sorted by (kick step, kick).
+    The schedule changes, the results do not: the default run and one in input order
+    (ZMPC_STRICT_ORDER=0, a subprocess) give bitwise the same histories — per-walk bounds and
+    the shared CoP, per-walk kick steps, a batch that is not a multiple of 64 — and the sorted
+    run needs no more wave passes for the same instance passes."""
+    import subprocess
+    import sys
+    B = 1000
+    zmax, zmin, x0, F, dt = synthetic_batch(B, 150, seed=21)
+    n = zmax.shape[1]
+    rng = np.random.default_rng(22)
+    F = rng.uniform(-800.0, 800.0, B)
+    ks = rng.integers(n // 4, 3 * n // 4, B).astype(np.int64)
+    if shared:  # one [n, 2] CoP for every walk (bounds stride 0)
+        zmax, zmin, x0 = zmax[0], zmin[0], np.zeros_like(x0)
+    inp = tmp_path / "in.npz"
+    np.savez(inp, zmax=zmax, zmin=zmin, x0=x0, kick=dt * F / M, ks=ks, dt=dt)
+    outs = []
+    for mode in ("1", "0"):
+        out = tmp_path / f"o{mode}.npz"
+        env = dict(os.environ, ZMPC_STRICT_ORDER=mode)
+        subprocess.run([sys.executable, "-c", _ORDER_CHILD, PKG, str(inp), str(out)], env=env,
+                       check=True, timeout=300)
+        outs.append(np.load(out))
+    srt, inorder = outs
+    assert int(np.abs(srt["st"]).max()) == 0 and int(np.abs(inorder["st"]).max()) == 0
+    assert np.array_equal(srt["h"], inorder["h"])
+    assert int(srt["ip"]) == int(inorder["ip"])
+    assert int(srt["wp"]) <= int(inorder["wp"])
+    # one walk of the batch against the oracle (per-walk kick step)
+    b = 777
+    zb, nb = (zmax, zmin) if shared else (zmax[b], zmin[b])
+    ref = O.rollout_strict(x0[b, 0], x0[b, 1], zb, nb, 150, dt, H, G, Q, R,
+                           kick=dt * F[b] / M, kick_step=int(ks[b]))
+    assert rmse(srt["h"][b, :, :, 0], ref[:, :, 0]) <= 1e-9
+
+
 def test_strict_work_counters():
     """zmpc_plan_counters: every solve takes at least one active-set pass; the working-set
     slots are a part of all pass-slots; reset zeroes them."""
