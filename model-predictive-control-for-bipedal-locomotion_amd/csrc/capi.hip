@@ -48,7 +48,7 @@ int launch_result(hipError_t e, const std::string& why, const char* what) {
 void free_plan(zmpc_plan* p) {
   if (!p) return;
   double* bufs[] = {p->p, p->Px, p->M,  p->L,     p->k,      p->kx,     p->kffa,
-                    p->X, p->G,  p->v,  p->Hz,    p->scanP,  p->fft_tw, p->fft_g};
+                    p->ksum, p->X, p->G,  p->v,  p->Hz,    p->scanP,  p->fft_tw, p->fft_g};
   for (double* b : bufs)
     if (b) (void)hipFree(b);
   if (p->info) (void)hipFree(p->info);
@@ -126,6 +126,7 @@ int zmpc_plan_create(int device, int32_t N, double T, double T2_2, double T3_6, 
     size_t n;
   } allocs[] = {{&P->p, (size_t)N},  {&P->Px, 3 * (size_t)N}, {&P->M, nn}, {&P->L, nn},
                 {&P->k, (size_t)P->Kpad + 64}, {&P->kx, 4}, {&P->kffa, 4 * (size_t)kffa_rows(N)},
+                {&P->ksum, (size_t)ksum_rows(N)},
                 {&P->scanP, kScanDoubles},
                 {&P->X, strict ? nn : 0}, {&P->G, strict ? nn : 0},
                 {&P->v, strict ? (size_t)N : 0}, {&P->Hz, strict ? nn : 0},

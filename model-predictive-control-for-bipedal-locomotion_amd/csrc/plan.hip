@@ -225,6 +225,24 @@ __global__ void zmpc_ffa_taps(int N, const double* __restrict__ k, double* __res
   t[4 * m + 3] = 0.0;
 }
 
+// 4c. suffix sums of the gain row for the rollout's sparse-difference correlation (rollout.hip,
+// axis_correlate_sparse): S_j = k_j + S_{j+1} from j = N − 1 down, laid out as ksum_rows says.
+// One wave; the sum is sequential in one lane (N ≤ 4096 additions, once per plan).
+__global__ void __launch_bounds__(64) zmpc_ksum(int N, const double* __restrict__ k,
+                                                double* __restrict__ t) {
+  const int lane = threadIdx.x;
+  for (int i = lane; i < ksum_rows(N); i += 64)
+    if ((i < 9 || i >= N + 8) && i != ksum_s0(N)) t[i] = 0.0;
+  if (lane == 0) {
+    double acc = 0.0;
+    for (int j = N - 1; j >= 1; --j) {
+      acc += k[j];
+      t[j + 8] = acc;
+    }
+    t[ksum_s0(N)] = acc + k[0];
+  }
+}
+
 // 4. y = M⁻¹ e0 by two blocked triangular solves (64-row blocks), then k = Pu y, kx = k·Px.
 // One 1024-thread workgroup.  Per block: the off-block part of every row's dot product is a
 // wave reduction over coalesced row (forward) / column-block (backward) reads, the 64×64
@@ -550,6 +568,8 @@ hipError_t zmpc_launch_plan(zmpc_plan* P, hipStream_t s, hipEvent_t* ev) {
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(zmpc_ffa_taps, dim3((kffa_rows(N) + 63) / 64), dim3(64), 0, s, N, P->k,
                      P->kffa);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(zmpc_ksum, dim3(1), dim3(64), 0, s, N, P->k, P->ksum);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   if ((e = mark(4)) != hipSuccess) return e;
   hipLaunchKernelGGL(zmpc_scan_matrices, dim3(1), dim3(64), 0, s, P->T, P->T2_2, P->T3_6, P->kx,

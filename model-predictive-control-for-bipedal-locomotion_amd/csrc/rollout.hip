@@ -198,6 +198,8 @@ struct RolloutArgs {
   const double2* fft_g;   // plan gain spectrum DFT(g)/P for this launch's P
   const double* kffa;     // plan fast-FIR taps [kffa_rows(N)][4] (axis_correlate_ffa)
   int kfm;                // fast-FIR steps per walk, ⌈(N+1)/2⌉ rounded up to the unroll
+  const double* ksum;     // plan suffix sums of k [ksum_rows(N)] (axis_correlate_sparse), or null
+  int hN;                 // horizon N (ksum layout)
 };
 
 // a 16-byte store with the non-temporal hint (streamed past the caches)
@@ -642,6 +644,66 @@ __device__ __forceinline__ void axis_correlate_ffa(const RolloutArgs& a,
   f[CW - 1] = A[NP] + Bo[NP];
 }
 
+// v_readlane of a double at a wave-uniform lane index
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+  const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, l);
+  const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), l);
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+
+// The correlation by summation by parts over the walk's z_ref changes.  With S_j = Σ_{j'≥j} k_j'
+// and d_m = z_ref[m+1] − z_ref[m],
+//   f_t = Σ_j k_j z_ref[t+1+j] = S_0 z_ref[t+1] + Σ_{j=1}^{N−1} S_j d_{t+j},
+// and the CoP references the footstep generators produce (cop_generator.py:34-115: one box per
+// support phase) are piecewise constant, so d is zero except at the support-phase switches —
+// ≈16 changes per axis in a 420-sample default.json walk against 150 taps per output.  The wave
+// finds its axis's changes with one ballot per chunk column (lane l tests m = l·CW + q), then
+// walks the set bits: every lane adds S_{m−t}·d_m to its CW outputs t (Ts = the plan's ksum
+// table staged in LDS; entries outside 1 ≤ j ≤ N−1 are zero, so lanes the change does not reach
+// read zeros at a clamped offset).  Exact for any input; a wave whose axis changes more than
+// kSparseMax times (dense bounds) returns false and takes the dense form instead.  Rounding
+// differs from the direct sum by ≈ε·Σ|S_j d_j| (test_sparse_correlation_equals_dense).
+constexpr int kSparseMax = 40;
+
+template <int CW>
+__device__ __forceinline__ bool axis_correlate_sparse(const RolloutArgs& a, const double* zr,
+                                                      const double* Ts, int lane, double* f) {
+  using ZL = ZrLayout<CW>;
+  const double* z = zr + ZL::idx(lane * CW);
+  double gv[CW + 1], d[CW];
+  unsigned long long mk[CW];
+  int cnt = 0;
+#pragma unroll
+  for (int j = 0; j <= CW; ++j) gv[j] = z[ZL::idx(j)];
+#pragma unroll
+  for (int q = 0; q < CW; ++q) {
+    d[q] = gv[q + 1] - gv[q];
+    mk[q] = __ballot(d[q] != 0.0);
+    cnt += __popcll(mk[q]);
+  }
+  if (cnt > kSparseMax) return false;
+  const int N = a.hN, s = lane * CW;
+  const double S0 = Ts[ksum_s0(N)];
+#pragma unroll
+  for (int r = 0; r < CW; ++r) f[r] = S0 * gv[r + 1];
+#pragma unroll
+  for (int q = 0; q < CW; ++q) {
+    unsigned long long m = mk[q];
+    while (m) {
+      const int L = __builtin_ctzll(m);
+      m &= m - 1;
+      const double dv = readlane_f64(d[q], L);
+      // f_{s+r} += S_{e−r} d with e = m − s, S_{e−r} = Ts[e − r + 8]
+      const int e = min(max(L * CW + q - s, 0), N + CW - 1);
+      const double* p = Ts + e + 9 - CW;
+#pragma unroll
+      for (int r = 0; r < CW; ++r) f[r] = fma(p[CW - 1 - r], dv, f[r]);
+    }
+  }
+  return true;
+}
+
 // Scan + replay + coalesced store of walk b's axis `axis` (f in registers); `stage` is the
 // walk's (dead) z_ref area, 2·lzp doubles, shared by both waves.
 template <int CW>
@@ -824,6 +886,10 @@ __device__ __forceinline__ void split_walk(const RolloutArgs& a, int64_t b, doub
     axis_load<CW>(a, b, tid, r);
     const double2 hl = reinterpret_cast<const double2*>(a.zmax + b * a.bstride)[n - 1];
     const double2 ll = reinterpret_cast<const double2*>(a.zmin + b * a.bstride)[n - 1];
+    // the plan's suffix-sum table (sparse-difference correlation) behind the two z_ref areas
+    double* Ts = smem + 2 * a.lzp;
+    if (a.ksum != nullptr)
+      for (int i = tid; i < ksum_rows(a.hN); i += 128) Ts[i] = a.ksum[i];
     if constexpr (PM) __builtin_amdgcn_s_setprio(0);
     // ---- 2. z_ref rows + window padding (zmp_controller.py:81-88) --------------------------
 #pragma unroll
@@ -843,7 +909,11 @@ __device__ __forceinline__ void split_walk(const RolloutArgs& a, int64_t b, doub
     }
     __syncthreads();
     // ---- 3. correlation (this wave's axis) -------------------------------------------------
-    if constexpr (FFA && (CW & 1))
+    // sparse z_ref differences (piecewise-constant CoP) first, else the dense forms
+    const bool sparse = a.ksum != nullptr && !(a.dbg & 1) &&
+                        axis_correlate_sparse<CW>(a, axis ? zr1 : zr0, Ts, lane, f);
+    if (sparse) {
+    } else if constexpr (FFA && (CW & 1))
       axis_correlate_ffa<CW>(a, kg, axis ? zr1 : zr0, lane, f);  // kg = the fast-FIR taps
     else
       axis_correlate<CW>(a, kg, axis ? zr1 : zr0, lane, f);  // k: wave-uniform scalar loads
@@ -1885,7 +1955,7 @@ void launch_chunk(hipStream_t s, const RolloutArgs& a0, int N) {
 }
 
 template <int CW>
-void launch_unc(const RolloutGeom& g, size_t lds, hipStream_t s, const RolloutArgs& a) {
+void launch_unc(const RolloutGeom& g, size_t lds, hipStream_t s, RolloutArgs a) {
   // Kernel choice; ZMPC_ROLLOUT_VARIANT overrides it for A/B runs (DESIGN.md §4 has the
   // config-2 measurements): 8 = split, persistent grid (default); 6 = split, one walk per
   // workgroup (both with the DPP lane scan; 15 / 16 the same with the shuffle scan); 1 =
@@ -1897,7 +1967,19 @@ void launch_unc(const RolloutGeom& g, size_t lds, hipStream_t s, const RolloutAr
     return e ? atoi(e) : 8;
   }();
   const size_t lds_axis = lds - (size_t)a.kcp * sizeof(double);  // no staged gain row
-  const size_t lds_split = std::max<size_t>(lds_axis, 6 * (size_t)a.n * sizeof(double));
+  size_t lds_split = std::max<size_t>(lds_axis, 6 * (size_t)a.n * sizeof(double));
+  // the sparse-difference correlation runs in the split-axis kernels (split_walk, one copy-out
+  // round) and stages the plan's suffix sums behind the z_ref areas
+  const bool split_family =
+      a.fsh == nullptr && g.passes == 1 && lds_split <= 64 * 1024 &&
+      (variant == 8 || variant == 6 || variant == 15 || variant == 16 || variant == 17 ||
+       variant == 18 || variant == 19);
+  const size_t lds_sparse =
+      std::max(lds_axis + (size_t)ksum_rows(a.hN) * sizeof(double), lds_split);
+  if (split_family && a.ksum != nullptr && lds_sparse <= 64 * 1024)
+    lds_split = lds_sparse;
+  else
+    a.ksum = nullptr;
   RolloutArgs b = a;
   if (a.fsh != nullptr) {
     // shared CoP, f precomputed: scan (DPP; variant 16: shuffles), replay and the history
@@ -2036,6 +2118,13 @@ hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, con
                 nullptr,      nullptr};
   a.kffa = p->kffa;
   a.kfm = g.kfm;
+  // ZMPC_SPARSE_CORR=0: dense correlation only (A/B and the equality tests)
+  static const bool sparse_corr = [] {
+    const char* e = getenv("ZMPC_SPARSE_CORR");
+    return !(e && atoi(e) == 0);
+  }();
+  a.ksum = sparse_corr ? p->ksum : nullptr;
+  a.hN = p->N;
   WideGeom wg;
   static const bool no_wide = getenv("ZMPC_ROLLOUT_NO_WIDE") != nullptr;  // A/B: chunk kernel
   if (g.passes > 1 && (no_wide || !wide_geom(p->N, n, &wg))) {

@@ -48,6 +48,8 @@ struct zmpc_plan {
   double* kx = nullptr;  // [3]  k·Px
   double* kffa = nullptr;  // [kffa_rows(N)][4] two-parallel fast-FIR taps of k (rollout.hip):
                            // (E_m, O_m, E_m + O_{m−1}, 0), E_m = k_{2m}, O_m = k_{2m+1}, zero past N
+  double* ksum = nullptr;  // [ksum_rows(N)] suffix sums of k for the sparse-difference
+                           // correlation (rollout.hip axis_correlate_sparse; layout at ksum_rows)
   double* scanP = nullptr;  // [8][kScanLevels][9] (Ā^C)^(2^r) rollout scan propagators, then
                             // [8][33][9] (Ā^C)^k (kScanPowOff)
   double* X = nullptr;   // [N,N] L⁻¹ Puᵀ (strict plans)
@@ -72,6 +74,12 @@ struct zmpc_plan {
 
 // rows of the fast-FIR tap table: m = 0..⌈(N+1)/2⌉−1, plus zero rows for an unrolled loop
 __host__ __device__ constexpr int kffa_rows(int N) { return (N + 2) / 2 + 8; }
+
+// suffix sums S_j = Σ_{j' ≥ j} k_{j'} of the gain row: entry i = S_{i−8} for 1 ≤ i − 8 ≤ N − 1,
+// zero elsewhere in [0, N + 16) (so a lane's 8-wide read at any clamped offset stays inside),
+// S_0 at N + 16
+__host__ __device__ constexpr int ksum_rows(int N) { return N + 18; }
+__host__ __device__ constexpr int ksum_s0(int N) { return N + 16; }
 
 constexpr int kFftPT = 8192;    // largest transform (twiddle table size)
 constexpr int kFftPmin = 256;   // smallest transform with a gain spectrum

@@ -456,6 +456,93 @@ def test_rollout_kernel_variants_agree(tmp_path):
         assert np.abs(outs[0] - o).max() <= 1e-12
 
 
+SPARSE_MAX = 40  # rollout.hip kSparseMax: more z_ref changes per axis take the dense form
+
+
+def _piecewise_walks(rng, B, n, changes):
+    """Piecewise-constant bounds with `changes` z_ref changes per axis at distinct random
+    samples (always including the first and the last possible one, m = 0 and m = n − 2)."""
+    zmax = np.empty((B, n, 2))
+    for b in range(B):
+        for ax in range(2):
+            k = min(changes, n - 1)
+            pos = rng.choice(np.arange(1, n - 2), size=max(k - 2, 0), replace=False) \
+                if n > 3 else np.array([], int)
+            pos = np.unique(np.concatenate([pos, [0, n - 2]]))[:k]
+            steps = np.zeros(n)
+            steps[pos + 1] = rng.uniform(-0.05, 0.05, pos.size)
+            zmax[b, :, ax] = 0.1 + np.cumsum(steps)
+    return zmax + 0.05, zmax - 0.05
+
+
+_SPARSE_CHILD = r"""
+import sys, numpy as np, torch
+sys.path.insert(0, sys.argv[1])
+from mpc_bipedal.solver import Plan
+d = np.load(sys.argv[2])
+p = Plan(0, int(d["N"]), float(d["dt"]), 0.75, 9.81, 1.0, 1e-6, False)
+h, st = p.rollout(d["zmax"], d["zmin"], d["x0"], kick=d["kick"], kick_step=int(d["ks"]))
+assert int(st.abs().max()) == 0
+np.save(sys.argv[3], h.cpu().numpy())
+"""
+
+
+@pytest.mark.parametrize("n", (2, 65, 350, 420, 513))
+def test_sparse_correlation_equals_dense(n, tmp_path):
+    """The sparse-difference correlation (rollout.hip axis_correlate_sparse, the default for
+    piecewise-constant CoP bounds) against the dense forms (ZMPC_SPARSE_CORR=0, a subprocess)
+    and the oracle, on one batch that mixes default.json walks with rigid offsets, random-walk
+    bounds (dense: the fallback), and piecewise-constant bounds with SPARSE_MAX − 1, SPARSE_MAX
+    and SPARSE_MAX + 1 changes per axis at random samples including m = 0 and m = n − 2, so
+    waves on both sides of the switch sit in one launch.  n covers odd and even chunk widths."""
+    import subprocess
+    import sys
+    N = 150
+    rng = np.random.default_rng(n)
+    cop = golden("walk_n150.npz")
+    dt = float(cop["dt"])
+    parts_hi, parts_lo = [], []
+    base = min(n, cop["zmax"].shape[0])
+    for _ in range(24):  # default CoP (its first n samples), rigid offsets
+        off = rng.uniform(-0.02, 0.02, (1, 2))
+        parts_hi.append(np.concatenate([cop["zmax"][:base], np.repeat(cop["zmax"][base - 1:base],
+                                                                      n - base, 0)]) + off)
+        parts_lo.append(np.concatenate([cop["zmin"][:base], np.repeat(cop["zmin"][base - 1:base],
+                                                                      n - base, 0)]) + off)
+    hi, lo = np.stack(parts_hi), np.stack(parts_lo)
+    ctr = np.cumsum(rng.normal(0, 0.01, (24, n, 2)), 1)  # dense
+    hi, lo = np.concatenate([hi, ctr + 0.05]), np.concatenate([lo, ctr - 0.05])
+    for c in (1, 2, SPARSE_MAX - 1, SPARSE_MAX, SPARSE_MAX + 1):
+        a, b = _piecewise_walks(rng, 8, n, c)
+        hi, lo = np.concatenate([hi, a]), np.concatenate([lo, b])
+    mixed_hi, mixed_lo = _piecewise_walks(rng, 8, n, 3)  # x sparse, y dense
+    mixed_hi[:, :, 1] = ctr[:8, :, 1] + 0.05
+    mixed_lo[:, :, 1] = ctr[:8, :, 1] - 0.05
+    zmax, zmin = np.concatenate([hi, mixed_hi]), np.concatenate([lo, mixed_lo])
+    B = zmax.shape[0]
+    x0 = np.zeros((B, 2, 3))
+    x0[:, :, 0] = rng.uniform(-0.01, 0.01, (B, 2))
+    kick = rng.uniform(0, 0.2, B)
+    ks = max(n // 3, 0)
+    inp = tmp_path / "in.npz"
+    np.savez(inp, zmax=zmax, zmin=zmin, x0=x0, kick=kick, ks=ks, dt=dt, N=N)
+    outs = {}
+    for mode in ("1", "0"):
+        out = tmp_path / f"h{mode}.npy"
+        env = dict(os.environ, ZMPC_SPARSE_CORR=mode)
+        subprocess.run([sys.executable, "-c", _SPARSE_CHILD, PKG, str(inp), str(out)], env=env,
+                       check=True, timeout=300)
+        outs[mode] = np.load(out)
+    scale = np.abs(outs["0"]).max(axis=1, keepdims=True) + 1.0
+    assert (np.abs(outs["1"] - outs["0"]) / scale).max() <= 1e-12
+    ref = O.rollout_gain(zmax, zmin, x0, N, dt, H, G, Q, R, kick, ks)
+    assert np.abs(outs["1"] - ref).max() <= 1e-8
+    # the default path in this process is the sparse one too
+    h, _ = plan(N, dt=dt).rollout(zmax, zmin, x0, kick=kick, kick_step=ks)
+    assert np.array_equal(h.cpu().numpy(), outs["1"]) or \
+        os.environ.get("ZMPC_SPARSE_CORR") == "0"
+
+
 def test_full_size_config2_properties():
     """BASELINE config 2 size (B=4096, N=150): oracle on a sample + translation invariance
     over the whole batch (x0 + δe0 and bounds + δ shift every position by δ exactly)."""
