@@ -57,6 +57,7 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
 FP64_PEAK_TFS = 78.6    # FP64 vector = matrix peak (spec)
 FP64_SUSTAINED_TFS = 56.6  # profiles/r1_fp64_peak.log: register-only FMA chains, 8 waves/SIMD
 SEED = 20251226
+SPARSE_MAX = 40  # rollout.hip kSparseMax: z_ref changes per axis the sparse correlation takes
 # strict_lq.hip FLOP per instance-slot of one active-set pass (fma = 2): working-set slot =
 # Riccati step 117 + forward 24 + costate 19; free-tail slot = s recursion 23 + forward 21
 STRICT_FLOP_WS = 160
@@ -815,6 +816,35 @@ def main():
             com_rmse_ref = float(np.sqrt(np.mean(
                 (hist[0, :, :, 0].cpu().numpy() - ref_com) ** 2)))
 
+    # the correlation form the rollout took: the sparse-difference form (rollout.hip
+    # axis_correlate_sparse) for waves whose axis has ≤ 40 z_ref changes, else dense.  The dense
+    # form is timed on the same inputs beside it (ZMPC_SPARSE_CORR=0, read per launch)
+    corr = None
+    if rank == 0 and not cfg.strict and not wl["shared"] and not P_fft:
+        zr = (zmax_h + zmin_h) / 2
+        ch = np.count_nonzero(np.diff(zr, axis=1), axis=1)  # [B, 2] changes per walk and axis
+        prev = os.environ.get("ZMPC_SPARSE_CORR")
+        os.environ["ZMPC_SPARSE_CORR"] = "0"
+        try:
+            for _ in range(max(1, args.warmup)):
+                launch()
+            torch.cuda.synchronize()
+            _, dense_ms = timed_region(launch, args.steps, 1, dev)
+        finally:
+            if prev is None:
+                os.environ.pop("ZMPC_SPARSE_CORR")
+            else:
+                os.environ["ZMPC_SPARSE_CORR"] = prev
+            launch()  # the history the rest of the run reads comes from the default form
+            torch.cuda.synchronize()
+        corr = {"form": "sparse-difference" if prev != "0" else "dense",
+                "sparse_max_changes_per_axis": SPARSE_MAX,
+                "zref_changes_per_axis_mean": float(ch.mean()),
+                "zref_changes_per_axis_max": int(ch.max()),
+                "walk_axes_sparse_frac": float((ch <= SPARSE_MAX).mean()),
+                "dense_kernel_ms": dense_ms,
+                "dense_hbm_frac": alg_bytes / (dense_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+
     gather_ms = None
     if world > 1:
         full, gather_ms = gather_com(hist[..., 0].contiguous(), B * world, world, dev)
@@ -933,6 +963,7 @@ def main():
             "allgather_ms": gather_ms,
             "pcie_inclusive": pcie,
             "pipelined": pipelined,
+            "correlation": corr,
             "plan": plan_rec,
         }
         print(json.dumps(line))

@@ -200,6 +200,8 @@ struct RolloutArgs {
   int kfm;                // fast-FIR steps per walk, ⌈(N+1)/2⌉ rounded up to the unroll
   const double* ksum;     // plan suffix sums of k [ksum_rows(N)] (axis_correlate_sparse), or null
   int hN;                 // horizon N (ksum layout)
+  int64_t pf_ahead;       // one walk per workgroup: touch walk b + pf_ahead's bounds (the next
+                          // dispatch round's) into the caches early; 0 = off
 };
 
 // a 16-byte store with the non-temporal hint (streamed past the caches)
@@ -869,6 +871,7 @@ __device__ __forceinline__ void split_walk(const RolloutArgs& a, int64_t b, doub
   const int tid = threadIdx.x, lane = tid & 63, axis = tid >> 6;
   const int n = a.n, nsteps = n - 1;
   double f[CW];
+  double pf0 = 0.0, pf1 = 0.0;  // prefetch results (kept alive to the end, never used)
   const double* xb = a.x0 + b * 6 + 3 * axis;
   const double xi[3] = {xb[0], xb[1], xb[2]};
   const double kk = (axis == 1 && a.kick != nullptr) ? a.kick[b] : 0.0;
@@ -890,6 +893,15 @@ __device__ __forceinline__ void split_walk(const RolloutArgs& a, int64_t b, doub
     double* Ts = smem + 2 * a.lzp;
     if (a.ksum != nullptr)
       for (int i = tid; i < ksum_rows(a.hN); i += 128) Ts[i] = a.ksum[i];
+    // the bounds of the walk the next dispatch round puts on this slot, one double per 64 B
+    // (threads 0..63 z_max, 64..127 z_min; two loads cover n ≤ 512 samples), so that round's
+    // loads hit L2 / Infinity Cache instead of HBM under this round's compute
+    if (a.pf_ahead > 0 && b + a.pf_ahead < a.B) {
+      const double* src = (tid < 64 ? a.zmax : a.zmin) + (b + a.pf_ahead) * a.bstride;
+      const int ln = tid & 63, nd = 2 * n;
+      pf0 = src[min(ln * 8, nd - 1)];
+      pf1 = src[min(ln * 8 + 512, nd - 1)];
+    }
     if constexpr (PM) __builtin_amdgcn_s_setprio(0);
     // ---- 2. z_ref rows + window padding (zmp_controller.py:81-88) --------------------------
 #pragma unroll
@@ -1062,6 +1074,7 @@ __device__ __forceinline__ void split_walk(const RolloutArgs& a, int64_t b, doub
     if (RND > 1 && rnd + 1 < RND) __syncthreads();  // staging read out before the next round
   }
   if (a.status != nullptr && tid == 0) a.status[b] = flag[0] | flag[1];
+  if (a.dbg < 0) hist[tid] = pf0 + pf1;  // never (dbg ≥ 0): keeps the prefetch loads
 }
 
 
@@ -1974,33 +1987,35 @@ void launch_unc(const RolloutGeom& g, size_t lds, hipStream_t s, RolloutArgs a) 
       a.fsh == nullptr && g.passes == 1 && lds_split <= 64 * 1024 &&
       (variant == 8 || variant == 6 || variant == 15 || variant == 16 || variant == 17 ||
        variant == 18 || variant == 19);
-  const size_t lds_sparse =
-      std::max(lds_axis + (size_t)ksum_rows(a.hN) * sizeof(double), lds_split);
+  const size_t lds_ks = lds_axis + (size_t)ksum_rows(a.hN) * sizeof(double);
+  const size_t lds_sparse = std::max(lds_ks, lds_split);
+  // two-round copy-out variants (11 / 12): half the staging rows
+  const size_t lds_h2 = std::max<size_t>(lds_axis, 6 * (size_t)((a.n + 1) / 2) * sizeof(double));
+  const bool rnd2 = a.fsh == nullptr && g.passes == 1 && (variant == 11 || variant == 12);
   if (split_family && a.ksum != nullptr && lds_sparse <= 64 * 1024)
     lds_split = lds_sparse;
-  else
+  else if (!(rnd2 && a.ksum != nullptr && std::max(lds_ks, lds_h2) <= 64 * 1024))
     a.ksum = nullptr;
+  const size_t lds_h = a.ksum != nullptr ? std::max(lds_ks, lds_h2) : lds_h2;
   RolloutArgs b = a;
   if (a.fsh != nullptr) {
     // shared CoP, f precomputed: scan (DPP; variant 16: shuffles), replay and the history
     // stores only
-    const size_t lds_h = 6 * (size_t)a.n * sizeof(double);
+    const size_t lds_f = 6 * (size_t)a.n * sizeof(double);
     if (variant == 16)
       hipLaunchKernelGGL((zmpc_rollout_unc_split_kernel<CW, true>), dim3((unsigned)a.B),
-                         dim3(128), lds_h, s, a);
+                         dim3(128), lds_f, s, a);
     else
       hipLaunchKernelGGL((zmpc_rollout_unc_splitd_kernel<CW, true>), dim3((unsigned)a.B),
-                         dim3(128), lds_h, s, a);
+                         dim3(128), lds_f, s, a);
     return;
   }
   if (g.passes == 1 && variant == 12) {
-    const size_t lds_h = std::max<size_t>(lds_axis, 6 * (size_t)((a.n + 1) / 2) * sizeof(double));
     hipLaunchKernelGGL(zmpc_rollout_unc_split2_kernel<CW>, dim3((unsigned)a.B), dim3(128), lds_h,
                        s, a);
     return;
   }
   if (g.passes == 1 && variant == 11) {
-    const size_t lds_h = std::max<size_t>(lds_axis, 6 * (size_t)((a.n + 1) / 2) * sizeof(double));
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
             &per_cu, reinterpret_cast<const void*>(zmpc_rollout_unc_pers2_kernel<CW>), 128,
@@ -2071,8 +2086,27 @@ void launch_unc(const RolloutGeom& g, size_t lds, hipStream_t s, RolloutArgs a) 
         hipLaunchKernelGGL(zmpc_rollout_unc_pers_kernel<CW>, dim3((unsigned)grid), dim3(128),
                            lds_split, s, a, a.k, a.scanP, a.kx, a.hist);
     } else if (dpp && ffa) {
+      // ZMPC_PREFETCH=0 turns the next-round bound prefetch off (A/B)
+      static const bool pf_on = [] {
+        const char* e = getenv("ZMPC_PREFETCH");
+        return !(e && atoi(e) == 0);
+      }();
+      static thread_local size_t occ_lds = 0;  // resident workgroups per CU, per LDS size
+      static thread_local int occ = 0;
+      if (pf_on && occ_lds != lds_split) {
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                &occ, reinterpret_cast<const void*>(zmpc_rollout_unc_splitd_kernel<CW>), 128,
+                lds_split) != hipSuccess)
+          occ = 0;
+        occ_lds = lds_split;
+      }
+      // only for two dispatch rounds (config 2: 29.6 → 26.9 µs); with more rounds the rounds
+      // drift apart and the touched lines are evicted before use (B = 16384: 92 → 117 µs)
+      RolloutArgs c = a;
+      const int64_t R = (int64_t)std::max(g_cus, 1) * occ;
+      c.pf_ahead = (pf_on && a.n <= 512 && R > 0 && a.B <= 2 * R) ? R : 0;
       hipLaunchKernelGGL(zmpc_rollout_unc_splitd_kernel<CW>, dim3((unsigned)a.B), dim3(128),
-                         lds_split, s, a);
+                         lds_split, s, c);
     } else if (dpp) {
       hipLaunchKernelGGL((zmpc_rollout_unc_splitd_kernel<CW, false, false>), dim3((unsigned)a.B),
                          dim3(128), lds_split, s, a);
@@ -2118,12 +2152,10 @@ hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, con
                 nullptr,      nullptr};
   a.kffa = p->kffa;
   a.kfm = g.kfm;
-  // ZMPC_SPARSE_CORR=0: dense correlation only (A/B and the equality tests)
-  static const bool sparse_corr = [] {
-    const char* e = getenv("ZMPC_SPARSE_CORR");
-    return !(e && atoi(e) == 0);
-  }();
-  a.ksum = sparse_corr ? p->ksum : nullptr;
+  // ZMPC_SPARSE_CORR=0: dense correlation only (A/B, the equality tests and bench.py's dense
+  // side measurement; read per launch so that one process can time both forms)
+  const char* sc = getenv("ZMPC_SPARSE_CORR");
+  a.ksum = (sc && atoi(sc) == 0) ? nullptr : p->ksum;
   a.hN = p->N;
   WideGeom wg;
   static const bool no_wide = getenv("ZMPC_ROLLOUT_NO_WIDE") != nullptr;  // A/B: chunk kernel

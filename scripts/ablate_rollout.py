@@ -13,8 +13,14 @@ from mpc_bipedal.solver import Plan
 B = int(sys.argv[1]); N = int(sys.argv[2]); n = int(sys.argv[3])
 p = Plan(0, N, 1.5 / N, 0.75, 9.81, 1.0, 1e-6, False)
 rng = np.random.default_rng(0)
-zc = np.cumsum(rng.normal(0, 0.01, (B, n, 2)), 1)
-zmax = torch.as_tensor(zc + 0.05, device="cuda"); zmin = torch.as_tensor(zc - 0.05, device="cuda")
+if os.environ.get("ABL_DATA") == "cop":  # default.json CoP + rigid offsets (the bench's data)
+    cop = np.load(os.path.join(os.environ["ROOT"], "tests", "golden", "walk_n150.npz"))
+    off = rng.uniform(-0.02, 0.02, (B, 1, 2))
+    zmax = torch.as_tensor(cop["zmax"][None, :n] + off, device="cuda")
+    zmin = torch.as_tensor(cop["zmin"][None, :n] + off, device="cuda")
+else:  # random-walk bounds (dense z_ref changes)
+    zc = np.cumsum(rng.normal(0, 0.01, (B, n, 2)), 1)
+    zmax = torch.as_tensor(zc + 0.05, device="cuda"); zmin = torch.as_tensor(zc - 0.05, device="cuda")
 x0 = torch.zeros((B, 2, 3), dtype=torch.float64, device="cuda")
 L = p.rollout_launcher(zmax, zmin, x0)
 for _ in range(3): L()
@@ -25,11 +31,12 @@ for a, b in ev:
 torch.cuda.synchronize()
 print(json.dumps(dict(B=B, N=N, n=n, dbg=os.environ.get("ZMPC_DEBUG_ROLLOUT", "0"),
                       variant=os.environ.get("ZMPC_ROLLOUT_VARIANT", "8"),
+                      data=os.environ.get("ABL_DATA", "randomwalk"),
                       us=float(np.median([a.elapsed_time(b) for a, b in ev])) * 1e3)))
 '''
 
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-env0 = dict(os.environ, PKG=os.path.join(root, "model-predictive-control-for-bipedal-locomotion_amd"))
+env0 = dict(os.environ, ROOT=root, PKG=os.path.join(root, "model-predictive-control-for-bipedal-locomotion_amd"))
 # usage: ablate_rollout.py [variants=8,6,1,2] [dbg bits=0,1,15] [B=1024,4096,16384]
 VARIANTS = (sys.argv[1] if len(sys.argv) > 1 else "8,6,1,2").split(",")
 DBG = [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "0,1,15").split(",")]
