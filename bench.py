@@ -58,6 +58,7 @@ FP64_PEAK_TFS = 78.6    # FP64 vector = matrix peak (spec)
 FP64_SUSTAINED_TFS = 56.6  # profiles/r1_fp64_peak.log: register-only FMA chains, 8 waves/SIMD
 SEED = 20251226
 SPARSE_MAX = 40  # rollout.hip kSparseMax: z_ref changes per axis the sparse correlation takes
+SPARSE_MAX_WIDE = 64  # kSparseMaxWide: the same for the wide kernel (walks > 513 samples)
 # strict_lq.hip FLOP per instance-slot of one active-set pass (fma = 2): working-set slot =
 # Riccati step 117 + forward 24 + costate 19; free-tail slot = s recursion 23 + forward 21
 STRICT_FLOP_WS = 160
@@ -104,7 +105,8 @@ def rollout_kernel_name(B, n, N, strict, shared=False):
     if shared and n - 1 <= 512 and 6 * n * 8 <= 64 * 1024:
         return "zmpc_rollout_unc_splitd_kernel<CW, true> (+ zmpc_shared_f_kernel)"
     if fft_transform(n, N):
-        return "zmpc_rollout_unc_wide_kernel<CW, W, E> (FFT correlation)"
+        return ("zmpc_rollout_unc_wide_kernel<CW, W, E> (sparse-difference correlation; FFT "
+                "for dense bounds)")
     if n - 1 <= 512:
         # chunk width as rollout.hip:pick_cw; odd widths take the fast-FIR correlation, one walk
         # per workgroup
@@ -820,9 +822,12 @@ def main():
     # axis_correlate_sparse) for waves whose axis has ≤ 40 z_ref changes, else dense.  The dense
     # form is timed on the same inputs beside it (ZMPC_SPARSE_CORR=0, read per launch)
     corr = None
-    if rank == 0 and not cfg.strict and not wl["shared"] and not P_fft:
+    if rank == 0 and not cfg.strict and not wl["shared"]:
         zr = (zmax_h + zmin_h) / 2
         ch = np.count_nonzero(np.diff(zr, axis=1), axis=1)  # [B, 2] changes per walk and axis
+        wide = n - 1 > 512  # wide kernel: its own limit, and a walk is sparse if both axes are
+        lim = SPARSE_MAX_WIDE if wide else SPARSE_MAX
+        sparse_frac = float((ch.max(axis=1) <= lim).mean() if wide else (ch <= lim).mean())
         prev = os.environ.get("ZMPC_SPARSE_CORR")
         os.environ["ZMPC_SPARSE_CORR"] = "0"
         try:
@@ -838,10 +843,10 @@ def main():
             launch()  # the history the rest of the run reads comes from the default form
             torch.cuda.synchronize()
         corr = {"form": "sparse-difference" if prev != "0" else "dense",
-                "sparse_max_changes_per_axis": SPARSE_MAX,
+                "sparse_max_changes_per_axis": lim,
                 "zref_changes_per_axis_mean": float(ch.mean()),
                 "zref_changes_per_axis_max": int(ch.max()),
-                "walk_axes_sparse_frac": float((ch <= SPARSE_MAX).mean()),
+                "sparse_frac": sparse_frac,
                 "dense_kernel_ms": dense_ms,
                 "dense_hbm_frac": alg_bytes / (dense_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
 

@@ -1496,6 +1496,76 @@ __device__ __forceinline__ void fft_correlate8(double2 (&v)[8], double2* buf,
   __syncthreads();
 }
 
+// The sparse-difference correlation (axis_correlate_sparse) for the wide kernel: the changes a
+// lane's outputs need lie up to N − 1 samples ahead, in other waves' ranges, so each axis's
+// changes go to an LDS list first (per-wave counts → prefix → positions, deterministic order)
+// and every lane walks its axis's list.  Returns false, uniformly over the workgroup, when
+// either axis has more than kSparseMaxWide changes (both axes then take the dense form: the FFT
+// correlates them together).  Both calls' barriers are reached by every thread.
+constexpr int kSparseMaxWide = 64;
+
+template <int CW, int W>
+__device__ __forceinline__ bool wide_correlate_sparse(const RolloutArgs& a, const double* zr,
+                                                      const double* Ts, double* ld, int* lm,
+                                                      int (*scnt)[W], int axis, int w, int lane,
+                                                      double* f) {
+  using ZL = ZrLayout<CW>;
+  const int s = (w * 64 + lane) * CW;
+  const double* z = zr + ZL::idx(s);
+  double gv[CW + 1], d[CW];
+  unsigned long long mk[CW];
+  int cnt = 0;
+#pragma unroll
+  for (int j = 0; j <= CW; ++j) gv[j] = z[ZL::idx(j)];
+#pragma unroll
+  for (int q = 0; q < CW; ++q) {
+    d[q] = gv[q + 1] - gv[q];
+    mk[q] = __ballot(d[q] != 0.0);
+    cnt += __popcll(mk[q]);
+  }
+  if (lane == 0) scnt[axis][w] = cnt;
+  __syncthreads();
+  int tot0 = 0, tot1 = 0, base = 0;
+#pragma unroll
+  for (int v = 0; v < W; ++v) {
+    tot0 += scnt[0][v];
+    tot1 += scnt[1][v];
+    if (v < w) base += scnt[axis][v];
+  }
+  if (tot0 > kSparseMaxWide || tot1 > kSparseMaxWide || (a.dbg & 1)) return false;
+  const unsigned long long lt = (1ull << lane) - 1ull;
+  double* la = ld + axis * kSparseMaxWide;
+  int* lma = lm + axis * kSparseMaxWide;
+#pragma unroll
+  for (int q = 0; q < CW; ++q) {
+    if ((mk[q] >> lane) & 1ull) {
+      const int pos = base + __popcll(mk[q] & lt);
+      la[pos] = d[q];
+      lma[pos] = s + q;
+    }
+    base += __popcll(mk[q]);
+  }
+  __syncthreads();
+  const int N = a.hN, tot = axis ? tot1 : tot0;
+  const double S0 = Ts[ksum_s0(N)];
+#pragma unroll
+  for (int r = 0; r < CW; ++r) f[r] = S0 * gv[r + 1];
+  for (int c = 0; c < tot; ++c) {
+    const int e = min(max(lma[c] - s, 0), N + CW - 1);
+    const double dv = la[c];
+    const double* p = Ts + e + 9 - CW;
+#pragma unroll
+    for (int r = 0; r < CW; ++r) f[r] = fma(p[CW - 1 - r], dv, f[r]);
+  }
+  return true;
+}
+
+// LDS doubles the wide kernel's sparse attempt adds behind the two z_ref areas: the suffix-sum
+// table, the two change lists (values, then int positions)
+__host__ __device__ constexpr int wide_sparse_doubles(int N) {
+  return ((ksum_rows(N) + 1) & ~1) + 2 * kSparseMaxWide + kSparseMaxWide;
+}
+
 // Long walks (64·8+1 < n ≤ 64·8·8+1): the split-axis structure widened to W waves per axis
 // (workgroup = 2·W waves; wave w of an axis owns timesteps [w·64·CW, (w+1)·64·CW)).  Each
 // wave scans its range from a zero state; the true start state of wave w is chained over the
@@ -1514,10 +1584,35 @@ __global__ void __launch_bounds__(128 * W, E == 4 ? 6 : 4) zmpc_rollout_unc_wide
   const int n = a.n, nsteps = n - 1;
   double* zr0 = smem;
   double* zr1 = zr0 + a.lzp;
+  __shared__ int scnt[2][W];  // per-wave z_ref change counts (sparse attempt)
+  double* Ts = smem + 2 * a.lzp;  // sparse attempt: suffix sums, then the change lists
+  double* ld = Ts + ((ksum_rows(a.hN) + 1) & ~1);
+  int* lm = reinterpret_cast<int*>(ld + 2 * kSparseMaxWide);
   // ---- 1. z_ref rows + window padding (zmp_controller.py:81-88) ----------------------------
   double f[CW];
   const int mbeg = (w * 64 + lane) * CW;
+  // the sparse-difference correlation first (piecewise-constant CoP), else the dense forms;
+  // the FFT form stages only the rows the change scan reads (its transform loads its own)
+  bool dense = true;
   if constexpr (E > 0) {
+    if (a.ksum != nullptr) {
+      const double2* zmx = reinterpret_cast<const double2*>(a.zmax + b * a.bstride);
+      const double2* zmn = reinterpret_cast<const double2*>(a.zmin + b * a.bstride);
+      const int lzs = W * 64 * CW + 1;
+      for (int i = tid; i < ksum_rows(a.hN); i += NT) Ts[i] = a.ksum[i];
+      for (int t = tid; t < lzs; t += NT) {
+        const int tc = min(t, n - 1);  // padding = last row
+        const double2 hi = zmx[tc], lo = zmn[tc];
+        zr0[ZL::idx(t)] = (hi.x + lo.x) / 2;
+        zr1[ZL::idx(t)] = (hi.y + lo.y) / 2;
+      }
+      __syncthreads();
+      dense = !wide_correlate_sparse<CW, W>(a, axis ? zr1 : zr0, Ts, ld, lm, scnt, axis, w, lane,
+                                             f);
+    }
+  }
+  if (!dense) {
+  } else if constexpr (E > 0) {
     // FFT correlation: s[t] = (z_x, z_y) for t < P (rows past n − 1: the last row)
     double2* buf = reinterpret_cast<double2*>(smem);
     const double2* zmx = reinterpret_cast<const double2*>(a.zmax + b * a.bstride);
@@ -1562,9 +1657,13 @@ __global__ void __launch_bounds__(128 * W, E == 4 ? 6 : 4) zmpc_rollout_unc_wide
         }
       }
     }
+    if (a.ksum != nullptr)
+      for (int i = tid; i < ksum_rows(a.hN); i += NT) Ts[i] = a.ksum[i];
     __syncthreads();
     // ---- 2. correlation ----------------------------------------------------------------------
-    axis_correlate<CW>(a, a.k, (axis ? zr1 : zr0) + ZL::idx(w * 64 * CW), lane, f);
+    if (a.ksum == nullptr ||
+        !wide_correlate_sparse<CW, W>(a, axis ? zr1 : zr0, Ts, ld, lm, scnt, axis, w, lane, f))
+      axis_correlate<CW>(a, a.k, (axis ? zr1 : zr0) + ZL::idx(w * 64 * CW), lane, f);
   }
   const double* xb = a.x0 + b * 6 + 3 * axis;
   const double xi[3] = {xb[0], xb[1], xb[2]};
@@ -2194,6 +2293,13 @@ hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, con
       q.fft_g = reinterpret_cast<const double2*>(p->fft_g) + (P - kFftPmin);
       lds_w = std::max(lds_w, (size_t)P * 16);
     }
+    // the sparse attempt's table and change lists behind the z_ref areas (within the default
+    // 64 KiB dynamic-LDS ceiling, else dense only)
+    const size_t lds_sp = (2 * (size_t)wg.lzp + wide_sparse_doubles(p->N)) * sizeof(double);
+    if (q.ksum != nullptr && lds_sp <= 64 * 1024)
+      lds_w = std::max(lds_w, lds_sp);
+    else
+      q.ksum = nullptr;
     switch (wg.w * 16 + wg.cw) {
 #define ZMPC_WCASE(W, C)                                                                         \
   case W * 16 + C:                                                                               \

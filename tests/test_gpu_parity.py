@@ -457,6 +457,7 @@ def test_rollout_kernel_variants_agree(tmp_path):
 
 
 SPARSE_MAX = 40  # rollout.hip kSparseMax: more z_ref changes per axis take the dense form
+SPARSE_MAX_WIDE = 64  # kSparseMaxWide: the wide kernel (walks of more than 513 samples)
 
 
 def _piecewise_walks(rng, B, n, changes):
@@ -487,20 +488,23 @@ np.save(sys.argv[3], h.cpu().numpy())
 """
 
 
-@pytest.mark.parametrize("n", (2, 65, 350, 420, 513))
-def test_sparse_correlation_equals_dense(n, tmp_path):
+@pytest.mark.parametrize("N,n", ((150, 2), (150, 65), (150, 350), (150, 420), (150, 513),
+                                 (512, 1431), (150, 1100), (256, 1000), (150, 2500)))
+def test_sparse_correlation_equals_dense(N, n, tmp_path):
     """The sparse-difference correlation (rollout.hip axis_correlate_sparse, the default for
     piecewise-constant CoP bounds) against the dense forms (ZMPC_SPARSE_CORR=0, a subprocess)
     and the oracle, on one batch that mixes default.json walks with rigid offsets, random-walk
     bounds (dense: the fallback), and piecewise-constant bounds with SPARSE_MAX − 1, SPARSE_MAX
     and SPARSE_MAX + 1 changes per axis at random samples including m = 0 and m = n − 2, so
-    waves on both sides of the switch sit in one launch.  n covers odd and even chunk widths."""
+    waves on both sides of the switch sit in one launch.  n covers odd and even chunk widths,
+    the split kernels (n ≤ 513) and the wide kernel's FFT and direct forms (longer walks, where
+    the limit is SPARSE_MAX_WIDE per axis and a walk is sparse only if both axes are)."""
     import subprocess
     import sys
-    N = 150
-    rng = np.random.default_rng(n)
+    rng = np.random.default_rng(n + N)
     cop = golden("walk_n150.npz")
-    dt = float(cop["dt"])
+    dt = 1.5 / N if N != 150 else float(cop["dt"])
+    lim = SPARSE_MAX if n <= 513 else SPARSE_MAX_WIDE
     parts_hi, parts_lo = [], []
     base = min(n, cop["zmax"].shape[0])
     for _ in range(24):  # default CoP (its first n samples), rigid offsets
@@ -512,7 +516,7 @@ def test_sparse_correlation_equals_dense(n, tmp_path):
     hi, lo = np.stack(parts_hi), np.stack(parts_lo)
     ctr = np.cumsum(rng.normal(0, 0.01, (24, n, 2)), 1)  # dense
     hi, lo = np.concatenate([hi, ctr + 0.05]), np.concatenate([lo, ctr - 0.05])
-    for c in (1, 2, SPARSE_MAX - 1, SPARSE_MAX, SPARSE_MAX + 1):
+    for c in (1, 2, lim - 1, lim, lim + 1):
         a, b = _piecewise_walks(rng, 8, n, c)
         hi, lo = np.concatenate([hi, a]), np.concatenate([lo, b])
     mixed_hi, mixed_lo = _piecewise_walks(rng, 8, n, 3)  # x sparse, y dense
