@@ -704,6 +704,9 @@ def main():
                          "run_compare_runtime.py:139; prints one line per horizon")
     ap.add_argument("--stub-solver", action="store_true",
                     help="CPU/gloo self-test of the multi-rank launcher (no GPU, no solver)")
+    ap.add_argument("--no-dense-leg", action="store_true",
+                    help="skip timing the dense correlation beside the default (profiles: the "
+                         "rocprof kernel average then covers the default launches only)")
     ap.add_argument("--pipelined", action="store_true",
                     help="also time batches pipelined two-deep on two streams (reported beside "
                          "value; off by default so a profile of the default command sees only "
@@ -822,7 +825,7 @@ def main():
     # axis_correlate_sparse) for waves whose axis has ≤ 40 z_ref changes, else dense.  The dense
     # form is timed on the same inputs beside it (ZMPC_SPARSE_CORR=0, read per launch)
     corr = None
-    if rank == 0 and not cfg.strict and not wl["shared"]:
+    if rank == 0 and not cfg.strict and not wl["shared"] and not args.no_dense_leg:
         zr = (zmax_h + zmin_h) / 2
         ch = np.count_nonzero(np.diff(zr, axis=1), axis=1)  # [B, 2] changes per walk and axis
         wide = n - 1 > 512  # wide kernel: its own limit, and a walk is sparse if both axes are

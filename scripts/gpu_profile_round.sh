@@ -9,7 +9,7 @@ TAG=${1:-round}
 WL=${2:-config2_n150_b4096}
 K=${3:-zmpc_rollout_unc}
 shift 3 2>/dev/null || shift $#
-ARGS="${*:---steps 20 --warmup 3} --no-cpu-baseline"
+ARGS="${*:---steps 20 --warmup 3} --no-cpu-baseline --no-dense-leg"
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
