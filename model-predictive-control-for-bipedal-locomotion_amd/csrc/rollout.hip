@@ -202,6 +202,7 @@ struct RolloutArgs {
   int hN;                 // horizon N (ksum layout)
   int64_t pf_ahead;       // one walk per workgroup: touch walk b + pf_ahead's bounds (the next
                           // dispatch round's) into the caches early; 0 = off
+  int pf_late;            // issue that prefetch after this walk's own loads have landed
 };
 
 // a 16-byte store with the non-temporal hint (streamed past the caches)
@@ -896,7 +897,7 @@ __device__ __forceinline__ void split_walk(const RolloutArgs& a, int64_t b, doub
     // the bounds of the walk the next dispatch round puts on this slot, one double per 64 B
     // (threads 0..63 z_max, 64..127 z_min; two loads cover n ≤ 512 samples), so that round's
     // loads hit L2 / Infinity Cache instead of HBM under this round's compute
-    if (a.pf_ahead > 0 && b + a.pf_ahead < a.B) {
+    if (!a.pf_late && a.pf_ahead > 0 && b + a.pf_ahead < a.B) {
       const double* src = (tid < 64 ? a.zmax : a.zmin) + (b + a.pf_ahead) * a.bstride;
       const int ln = tid & 63, nd = 2 * n;
       pf0 = src[min(ln * 8, nd - 1)];
@@ -920,6 +921,13 @@ __device__ __forceinline__ void split_walk(const RolloutArgs& a, int64_t b, doub
       }
     }
     __syncthreads();
+    if (a.pf_late && a.pf_ahead > 0 && b + a.pf_ahead < a.B) {
+      // (A/B) the same prefetch issued once this walk's own loads have landed
+      const double* src = (tid < 64 ? a.zmax : a.zmin) + (b + a.pf_ahead) * a.bstride;
+      const int ln = tid & 63, nd = 2 * n;
+      pf0 = src[min(ln * 8, nd - 1)];
+      pf1 = src[min(ln * 8 + 512, nd - 1)];
+    }
     // ---- 3. correlation (this wave's axis) -------------------------------------------------
     // sparse z_ref differences (piecewise-constant CoP) first, else the dense forms
     const bool sparse = a.ksum != nullptr && !(a.dbg & 1) &&
@@ -2186,10 +2194,11 @@ void launch_unc(const RolloutGeom& g, size_t lds, hipStream_t s, RolloutArgs a) 
                            lds_split, s, a, a.k, a.scanP, a.kx, a.hist);
     } else if (dpp && ffa) {
       // ZMPC_PREFETCH=0 turns the next-round bound prefetch off (A/B)
-      static const bool pf_on = [] {
+      static const int pf_mode = [] {
         const char* e = getenv("ZMPC_PREFETCH");
-        return !(e && atoi(e) == 0);
+        return e ? atoi(e) : 1;
       }();
+      const bool pf_on = pf_mode != 0;
       static thread_local size_t occ_lds = 0;  // resident workgroups per CU, per LDS size
       static thread_local int occ = 0;
       if (pf_on && occ_lds != lds_split) {
@@ -2204,6 +2213,7 @@ void launch_unc(const RolloutGeom& g, size_t lds, hipStream_t s, RolloutArgs a) 
       RolloutArgs c = a;
       const int64_t R = (int64_t)std::max(g_cus, 1) * occ;
       c.pf_ahead = (pf_on && a.n <= 512 && R > 0 && a.B <= 2 * R) ? R : 0;
+      c.pf_late = pf_mode == 2;
       hipLaunchKernelGGL(zmpc_rollout_unc_splitd_kernel<CW>, dim3((unsigned)a.B), dim3(128),
                          lds_split, s, c);
     } else if (dpp) {
