@@ -2118,8 +2118,20 @@ void launch_unc(const RolloutGeom& g, size_t lds, hipStream_t s, RolloutArgs a) 
     return;
   }
   if (g.passes == 1 && variant == 12) {
+    // (A/B) with the next-round prefetch as the default kernel takes it
+    const char* pe = getenv("ZMPC_PREFETCH");
+    const int pm = pe ? atoi(pe) : 1;
+    int occ12 = 0;
+    if (pm != 0 && hipOccupancyMaxActiveBlocksPerMultiprocessor(
+                       &occ12, reinterpret_cast<const void*>(zmpc_rollout_unc_split2_kernel<CW>),
+                       128, lds_h) != hipSuccess)
+      occ12 = 0;
+    const int64_t R12 = (int64_t)std::max(g_cus, 1) * occ12;
+    RolloutArgs c = a;
+    c.pf_ahead = (pm != 0 && a.n <= 512 && R12 > 0 && a.B <= 2 * R12) ? R12 : 0;
+    c.pf_late = pm == 2;
     hipLaunchKernelGGL(zmpc_rollout_unc_split2_kernel<CW>, dim3((unsigned)a.B), dim3(128), lds_h,
-                       s, a);
+                       s, c);
     return;
   }
   if (g.passes == 1 && variant == 11) {
