@@ -1599,6 +1599,15 @@ __global__ void __launch_bounds__(128 * W, E == 4 ? 6 : 4) zmpc_rollout_unc_wide
   // ---- 1. z_ref rows + window padding (zmp_controller.py:81-88) ----------------------------
   double f[CW];
   const int mbeg = (w * 64 + lane) * CW;
+  // next-dispatch-round prefetch (as split_walk): one double per 64 B of walk b + pf_ahead's
+  // bounds, results kept alive to the end and never used
+  double pf0 = 0.0, pf1 = 0.0;
+  if (a.pf_ahead > 0 && b + a.pf_ahead < a.B) {
+    const int nd = 2 * n, half = NT / 2, tl = tid % half;
+    const double* src = (tid < half ? a.zmax : a.zmin) + (b + a.pf_ahead) * a.bstride;
+    pf0 = src[min(tl * 8, nd - 1)];
+    pf1 = src[min((tl + half) * 8, nd - 1)];
+  }
   // the sparse-difference correlation first (piecewise-constant CoP), else the dense forms;
   // the FFT form stages only the rows the change scan reads (its transform loads its own)
   bool dense = true;
@@ -1818,6 +1827,7 @@ __global__ void __launch_bounds__(128 * W, E == 4 ? 6 : 4) zmpc_rollout_unc_wide
       a.status[b] = fl;
     }
   }
+  if (a.dbg < 0) a.hist[tid] = pf0 + pf1;  // never (dbg ≥ 0): keeps the prefetch loads
 }
 
 // Geometry of the wide kernel: W waves per axis (2, 4 or 8), CW = ceil((n−1)/(64·W)) ≤ 8.
@@ -2074,6 +2084,29 @@ void launch_chunk(hipStream_t s, const RolloutArgs& a0, int N) {
                      chunk_lds_bytes(g), s, a, g.lc);
 }
 
+// The wide kernel, with the next-dispatch-round prefetch when the batch takes at most
+// ZMPC_PF_ROUNDS (default 2) rounds of resident workgroups.
+template <int C, int W, int E>
+void launch_wide(hipStream_t s, RolloutArgs q, size_t lds, int64_t B) {
+  static const int pf_rounds = [] {
+    const char* e = getenv("ZMPC_PF_ROUNDS");
+    return e ? atoi(e) : 2;
+  }();
+  static thread_local size_t occ_lds = 0;
+  static thread_local int occ = 0;
+  if (pf_rounds > 1 && occ_lds != lds) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &occ, reinterpret_cast<const void*>(zmpc_rollout_unc_wide_kernel<C, W, E>), 128 * W,
+            lds) != hipSuccess)
+      occ = 0;
+    occ_lds = lds;
+  }
+  const int64_t R = (int64_t)std::max(g_cus, 1) * occ;
+  q.pf_ahead = (pf_rounds > 1 && R > 0 && q.n <= 512 * W && B <= pf_rounds * R) ? R : 0;
+  hipLaunchKernelGGL((zmpc_rollout_unc_wide_kernel<C, W, E>), dim3((unsigned)B), dim3(128 * W),
+                     lds, s, q);
+}
+
 template <int CW>
 void launch_unc(const RolloutGeom& g, size_t lds, hipStream_t s, RolloutArgs a) {
   // Kernel choice; ZMPC_ROLLOUT_VARIANT overrides it for A/B runs (DESIGN.md §4 has the
@@ -2323,17 +2356,14 @@ hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, con
     else
       q.ksum = nullptr;
     switch (wg.w * 16 + wg.cw) {
-#define ZMPC_WCASE(W, C)                                                                         \
-  case W * 16 + C:                                                                               \
-    if (E == 4)                                                                                  \
-      hipLaunchKernelGGL((zmpc_rollout_unc_wide_kernel<C, W, 4>), dim3((unsigned)B),            \
-                         dim3(128 * W), lds_w, s, q);                                            \
-    else if (E == 8)                                                                             \
-      hipLaunchKernelGGL((zmpc_rollout_unc_wide_kernel<C, W, 8>), dim3((unsigned)B),            \
-                         dim3(128 * W), lds_w, s, q);                                            \
-    else                                                                                         \
-      hipLaunchKernelGGL((zmpc_rollout_unc_wide_kernel<C, W>), dim3((unsigned)B), dim3(128 * W), \
-                         lds_w, s, q);                                                           \
+#define ZMPC_WCASE(W, C)                          \
+  case W * 16 + C:                                \
+    if (E == 4)                                   \
+      launch_wide<C, W, 4>(s, q, lds_w, B);       \
+    else if (E == 8)                              \
+      launch_wide<C, W, 8>(s, q, lds_w, B);       \
+    else                                          \
+      launch_wide<C, W, 0>(s, q, lds_w, B);       \
     break;
       ZMPC_WCASE(2, 5) ZMPC_WCASE(2, 6) ZMPC_WCASE(2, 7) ZMPC_WCASE(2, 8)
       ZMPC_WCASE(4, 5) ZMPC_WCASE(4, 6) ZMPC_WCASE(4, 7) ZMPC_WCASE(4, 8)
