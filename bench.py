@@ -194,7 +194,7 @@ def herdt_bench(args, rank, world, dev):
                    "parallelism": f"dp{world}", "max_footsteps_in_window": mmax,
                    "solve": "one joint x/y QP (predict_herdt_joint, zmp_controller.py:533-826)"},
         "roofline": {"bound": "mfma", "achieved": tfs, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
-                     "frac": tfs / FP64_PEAK_TFS, "traffic": None,
+                     "frac": tfs / FP64_PEAK_TFS, "traffic": pmc_traffic(f"config6_n{N}_b{B}"),
                      "kernel": "zmpc_herdt_kernel", "kernel_ms": kern_ms,
                      "alg_flops_per_launch": flops,
                      "passes_per_solve": passes_per_solve,
