@@ -59,6 +59,7 @@ struct LqArgs {
   int toff;              // window slot k reads time i + toff + k (1 rollout, 0 step)
   int window_mode;
   int drift;             // max timesteps a lane may run ahead of its wave's slowest lane
+  int warm_free_term;    // warm start: slot N−2 (the previous solve's terminal slot) starts free
   int64_t n;             // samples per walk (rollout; 1 in window mode)
   int64_t nsteps;        // timesteps (n − 1, or 1)
   int64_t B;             // walks (rollout) or instances (step)
@@ -882,6 +883,12 @@ __global__ void __launch_bounds__(64 * G, W)
 #pragma unroll 8
             for (int k = 0; k < N - 1; ++k) fl.p[k * 64 + lane] = fl.p[(k + 1) * 64 + lane];
           }
+          // the previous solve's terminal slot is no longer terminal: it starts free (its end
+          // effect pinned it more often than the next solve keeps it; a CPU simulation of this
+          // iteration on the default walk's y axis at F_ext 0/400/800 N: 1.387 → 1.310 passes
+          // per solve).  Slot N−1 keeps the copy.  The converged set, hence the solution, is
+          // the same; only the passes to reach it change.
+          if (a.warm_free_term && N >= 2) fl.set(N - 2, lane, 0);
           klast = (kl >= N - 1) ? N - 1 : max(kl - 1, -1);
         } else {
           active = false;
@@ -1079,6 +1086,13 @@ void fill_consts(const zmpc_plan* p, LqArgs& a) {
     return e ? atoi(e) : 4;
   }();
   a.drift = drift;
+  static const int warm = [] {
+    // warm start of the shifted slot N−2 (the old terminal slot): 1 = free (default), 0 = kept
+    // as the shift leaves it (A/B)
+    const char* e = getenv("ZMPC_STRICT_WARM");
+    return e ? atoi(e) : 1;
+  }();
+  a.warm_free_term = warm;
   a.cnt = p->lqcnt;
   static const int dbg = [] {
     const char* e = getenv("ZMPC_DEBUG_LQ");
