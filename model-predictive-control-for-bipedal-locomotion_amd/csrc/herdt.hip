@@ -78,6 +78,9 @@ struct HerdtArgs {
   double* ws;            // per-wave slab [waves][N][NF][64]
   int nf;                // doubles per row in the slab
   unsigned long long* cnt;  // plan work counters [4..7] (zmpc_plan_counters), may be null
+  int warm;                 // warm start of the last rows (ZMPC_HERDT_WARM, A/B): 0 = row N−1
+                            // free (round 2), 1 = row N−2 free and row N−1 a copy, 2 = row N−1 a
+                            // copy (default), 3 / 4 = the last 2 / 3 rows unshifted
   unsigned long long* prof; // diagnostics (ZMPC_HERDT_PROF): clock per phase, summed; null
 };
 
@@ -873,8 +876,16 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
       a.foot[(wc * a.n + i + 1) * 2 + axis] = fc;
     }
     // warm start: the converged set shifted one row towards the present
+    // (round 3, config 6: row N−1 a copy of the old last row instead of free — 1.316 → 1.157
+    // passes per solve, 86.4 → 78.6 ms; the converged set and the solution do not change)
+    const unsigned char wlast = wset[(N - 1) * 64 + lane];
+    const unsigned char wl2 = N >= 2 ? wset[(N - 2) * 64 + lane] : 0;
+    const unsigned char wl3 = N >= 3 ? wset[(N - 3) * 64 + lane] : 0;
     for (int k = 0; k < N - 1; ++k) wset[k * 64 + lane] = wset[(k + 1) * 64 + lane];
-    wset[(N - 1) * 64 + lane] = 0;
+    wset[(N - 1) * 64 + lane] = a.warm == 0 ? 0 : wlast;
+    if (a.warm == 1 && N >= 2) wset[(N - 2) * 64 + lane] = 0;
+    if (a.warm >= 3 && N >= 2) wset[(N - 2) * 64 + lane] = wl2;
+    if (a.warm >= 4 && N >= 3) wset[(N - 3) * 64 + lane] = wl3;
   }
   if (valid && a.status != nullptr) {
     const int other = __shfl(fq, lane ^ 1, 64);
@@ -969,6 +980,11 @@ hipError_t zmpc_launch_herdt(const zmpc_plan* p, const zmpc_herdt_params* prm, i
   }();
   if (prof) (void)hipMemsetAsync(prof, 0, 8 * sizeof(unsigned long long), s);
   a.prof = prof;
+  static const int warm = [] {
+    const char* e = getenv("ZMPC_HERDT_WARM");
+    return e ? atoi(e) : 2;
+  }();
+  a.warm = warm;
   const int mm = prm->max_footsteps;
   const int MM = mm <= 2 ? 2 : mm <= 4 ? 4 : mm <= 6 ? 6 : mm <= 7 ? 7 : mm <= 8 ? 8 : 0;
   if (MM == 0) {
