@@ -10,7 +10,9 @@ Warm starts (W = the previous timestep's converged set, N slots):
   c  as b, slots N−2 and N−1 free
   d  as b, slot N−2 (the old terminal slot) free   — the kernel's default since round 3
   f  as b, slot N−2 takes the old slot N−2
-Measured here: b 1.387, a 1.495, c 1.517, d 1.310, f 1.325 passes per solve.
+  g  as d, slot N−3 free too
+  h  as d, slot N−1 takes the old slot N−2
+Measured here: b 1.387, a 1.495, c 1.517, d 1.310, f 1.325, g 1.325, h 1.531 passes per solve.
 
 usage: python scripts/strict_warm_sim.py [modes, default "b,d"]
 """
@@ -54,6 +56,10 @@ def warm(W, mode):
         W0[-2] = 0
     if mode == "f":
         W0[-2] = W[-2]
+    if mode == "g":  # d, and slot N−3 free too
+        W0[-2] = W0[-3] = 0
+    if mode == "h":  # d, slot N−1 takes the old pre-terminal slot
+        W0[-2], W0[-1] = 0, W[-2]
     return W0
 
 
