@@ -1107,7 +1107,11 @@ hipError_t launch_lq(const zmpc_plan* p, LqArgs& a, int64_t waves, hipStream_t s
   const int64_t blocks = (waves + var.G - 1) / var.G;
   const size_t lds = lq_lds_bytes(var, p->N);
   // rollouts over per-walk bounds: non-temporal checkpoints (see CkIO)
-  const bool nt = !a.window_mode && !a.shared;
+  static const int nt_env = [] {  // A/B only: 0 / 1 force cached / non-temporal checkpoints
+    const char* e = getenv("ZMPC_STRICT_NT");
+    return e ? atoi(e) : -1;
+  }();
+  const bool nt = nt_env >= 0 ? nt_env == 1 : (!a.window_mode && !a.shared);
   hipLaunchKernelGGL(nt ? var.kernel_nt : var.kernel, dim3((unsigned)blocks), dim3(64 * var.G),
                      lds, s, a, (const double*)p->lqtab);
   hipError_t e = hipGetLastError();
