@@ -119,7 +119,7 @@ def rollout_kernel_name(B, n, N, strict, shared=False):
     return "zmpc_rollout_unc_wide_kernel" if n - 1 <= 4096 else "zmpc_rollout_unc_chunk_kernel"
 
 
-def herdt_bench(args, rank, world, dev):
+def herdt_bench(args, rank, world, dev, dist_on):
     """config 6: batched Herdt rollouts (csrc/herdt.hip); returns the JSON line (rank 0)."""
     from mpc_bipedal.controllers import herdt as H
     from mpc_bipedal.generators import SpeedTrajectoryGenerator
@@ -154,7 +154,7 @@ def herdt_bench(args, rank, world, dev):
     for _ in range(args.warmup):
         launch()
     plan.counters(reset=True)
-    elapsed, kern_ms = timed_region(launch, args.steps, world, dev)
+    elapsed, kern_ms = timed_region(launch, args.steps, dist_on, dev)
     cnt = plan.counters(reset=True)
     hist, foot, status = last["out"]
     assert int(status.abs().max()) == 0, "solver reported a failed instance"
@@ -354,6 +354,16 @@ def cpu_baseline(zmax_b, zmin_b, x0_b, kick_b, hist_gpu, cfg, budget_s):
                   seconds=s_el, com_rmse_gpu_vs_port=s_rms)
     out = dict(multi) if multi else dict(single)
     out["single_process"] = single
+    # §8d(i): one process at the default BLAS thread count (no thread limit)
+    sd = _cpu_walks(O, _walk_payload(zmax_b, zmin_b, x0_b, kick_b, hist_gpu,
+                                     range(first, len(x0_b))), cfg, budget_s)
+    out["single_process_default_blas"] = dict(
+        value=sd[0] / sd[1], unit="QP solves/s", cores=P, kind="port",
+        sample=f"{sd[2]} walk(s) = {sd[0]} solves of this batch, {_port_what(cfg)}, 1 process "
+               "at the default BLAS thread count", seconds=sd[1], com_rmse_gpu_vs_port=sd[3])
+    if cfg.strict:
+        out["optimized"] = _strict_optimized_leg(zmax_b, zmin_b, x0_b, kick_b, hist_gpu, cfg,
+                                                 budget_s, P)
     if not cfg.strict:
         nb = min(64, len(x0_b))
         zx = zmax_b if zmax_b.ndim == 3 else np.broadcast_to(zmax_b, (nb,) + zmax_b.shape)
@@ -372,6 +382,38 @@ def cpu_baseline(zmax_b, zmin_b, x0_b, kick_b, hist_gpu, cfg, budget_s):
             "com_rmse": float(np.sqrt(np.mean((hist_gpu[:nb, :, :, 0] - ref[..., 0]) ** 2))),
             "max_abs_state": float(np.abs(hist_gpu[:nb] - ref).max())}
     return out
+
+
+def _strict_optimized_leg(zmax_b, zmin_b, x0_b, kick_b, hist_gpu, cfg, budget_s, P):
+    """Optimized strict CPU leg: the device kernel's algorithm (LQ Riccati per working set +
+    primal-dual active set, warm-started) restated in C (oracle/strict_lq_cpu.c), OpenMP over
+    (walk, axis) instances on P cores, over whole walks of this batch — as many as ≈budget_s
+    of wall time allows (a probe of P walks sizes the sample)."""
+    from oracle import strict_cpu as SC
+    n = zmax_b.shape[-2]
+    Bt = len(x0_b)
+
+    def run(idx):
+        zx = zmax_b if zmax_b.ndim == 2 else zmax_b[idx]
+        zn = zmin_b if zmin_b.ndim == 2 else zmin_b[idx]
+        t0 = time.perf_counter()
+        h, st, ps = SC.rollout_strict(zx, zn, x0_b[idx], cfg.horizon, cfg.dt, cfg.h, cfg.g,
+                                      cfg.Q, cfg.R, kick=kick_b[idx], kick_step=n // 2,
+                                      threads=P)
+        return time.perf_counter() - t0, h, st, ps
+    probe = np.arange(min(P, Bt))
+    tp, _, _, _ = run(probe)
+    m = int(min(Bt, max(len(probe), budget_s / max(tp, 1e-6) * len(probe))))
+    idx = np.arange(m)
+    el, h, st, ps = run(idx)
+    solves = m * (n - 1) * 2
+    com = hist_gpu[idx, :, :, 0]
+    return {"value": solves / el, "unit": "QP solves/s", "cores": P, "kind": "port",
+            "sample": f"walks 0..{m - 1} of this batch ({solves} solves), the kernel's LQ "
+                      f"active-set algorithm in C (oracle/strict_lq_cpu.c), OpenMP on {P} "
+                      "threads", "seconds": el,
+            "passes_per_solve": float(ps.sum()) / solves, "status_max": int(st.max()),
+            "com_rmse_gpu_vs_port": float(np.sqrt(np.mean((h[..., 0] - com) ** 2)))}
 
 
 def _port_what(cfg):
@@ -483,14 +525,16 @@ def spawn_ranks(gpus, argv):
     return rc
 
 
-def timed_region(launch, steps, world, dev):
+def timed_region(launch, steps, collective, dev):
     """The bench contract's timed region: barrier + sync on both sides of exactly `steps`
-    launches, the job time = max over ranks.  Returns (elapsed seconds, average launch duration
-    in ms from one HIP event pair on the launch stream — None on CPU)."""
+    launches, the job time = max over ranks (collective: the process group's barrier and MAX
+    all-reduce — RCCL on device tensors with the nccl backend — run even at world size 1 under
+    --force-dist).  Returns (elapsed seconds, average launch duration in ms from one HIP event
+    pair on the launch stream — None on CPU)."""
     cuda = dev.type == "cuda"
     sync = torch.cuda.synchronize if cuda else (lambda: None)
     sync()
-    if world > 1:
+    if collective:
         dist.barrier()
     sync()
     if cuda:
@@ -510,7 +554,7 @@ def timed_region(launch, steps, world, dev):
     # this rank's time from the common start to its last launch finishing; the job time is the
     # max over ranks, so the closing barrier's own latency is not charged
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if collective:
         dist.barrier()
         t = torch.tensor([elapsed], dtype=torch.float64,
                          device=dev if dist.get_backend() == "nccl" else "cpu")
@@ -551,7 +595,7 @@ def stub_bench(args, rank, world):
         hist[:] = (idx + torch.arange(n, dtype=torch.float64)[None] / 1000.0)[..., None, None]
     for _ in range(args.warmup):
         launch()
-    elapsed, _ = timed_region(launch, args.steps, world, dev)
+    elapsed, _ = timed_region(launch, args.steps, world > 1, dev)
     full, gather_ms = gather_com(hist[..., 0].contiguous(), total, world, dev)
     expect = (torch.arange(total, dtype=torch.float64)[:, None] +
               torch.arange(n, dtype=torch.float64)[None] / 1000.0)[..., None]
@@ -640,7 +684,7 @@ def sweep_horizon(args, dev):
             launch = plan.rollout_launcher(zmax, zmin, x0, kick=kick, kick_step=n // 2)
             launch()
             steps = 3 if strict else 10
-            elapsed, kern_ms = timed_region(launch, steps, 1, dev)
+            elapsed, kern_ms = timed_region(launch, steps, False, dev)
             assert int(launch.status.abs().max()) == 0
             tag = "strict" if strict else "unc"
             row[f"gpu_batched_{tag}"] = B * (n - 1) * 2 * steps / elapsed
@@ -699,6 +743,10 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
                     help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo only to "
                          "rehearse several ranks on fewer GPUs)")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="initialise the process group even at --gpus 1, so that the "
+                         "multi-rank path (barrier, MAX all-reduce, CoM all-gather) runs through "
+                         "RCCL on one GPU")
     ap.add_argument("--sweep-horizon", default=None, metavar="LO:HI:STEP",
                     help="horizon sweep of the reference harness (e.g. 10:300:10), "
                          "run_compare_runtime.py:139; prints one line per horizon")
@@ -731,12 +779,16 @@ def main():
         if world > 1:
             dist.destroy_process_group()
         sys.exit(0 if ok else 1)
-    if world > 1:
+    dist_on = world > 1 or args.force_dist
+    if dist_on:
         ndev = torch.cuda.device_count()
         if local >= ndev and args.dist_backend == "nccl":
             raise SystemExit(f"rank {rank}: LOCAL_RANK {local} but only {ndev} GPU(s) visible")
         local %= ndev  # gloo rehearsal may put several ranks on one GPU
         torch.cuda.set_device(local)
+        if "MASTER_ADDR" not in os.environ:  # --force-dist without a launcher: a group of one
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
+                              RANK="0", WORLD_SIZE="1")
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
@@ -746,17 +798,17 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
     if args.sweep_horizon:
-        if world > 1:
+        if dist_on:
             raise SystemExit("--sweep-horizon runs on one GPU")
         sweep_horizon(args, dev)
         return
 
     conf = 3 if args.strict else args.config
     if CONFIGS[conf].get("herdt"):
-        line = herdt_bench(args, rank, world, dev)
+        line = herdt_bench(args, rank, world, dev, dist_on)
         if rank == 0:
             print(json.dumps(line))
-        if world > 1:
+        if dist_on:
             dist.destroy_process_group()
         return
     wl = dict(CONFIGS[conf])
@@ -787,7 +839,7 @@ def main():
     torch.cuda.synchronize()
     if cfg.strict:
         plan.counters(reset=True)  # count the timed launches only
-    elapsed, kern_ms = timed_region(launch, args.steps, world, dev)
+    elapsed, kern_ms = timed_region(launch, args.steps, dist_on, dev)
     work = plan.counters() if cfg.strict else None
     assert int(status.abs().max()) == 0, "solver reported a failed instance"
 
@@ -837,7 +889,7 @@ def main():
             for _ in range(max(1, args.warmup)):
                 launch()
             torch.cuda.synchronize()
-            _, dense_ms = timed_region(launch, args.steps, 1, dev)
+            _, dense_ms = timed_region(launch, args.steps, False, dev)
         finally:
             if prev is None:
                 os.environ.pop("ZMPC_SPARSE_CORR")
@@ -854,9 +906,14 @@ def main():
                 "dense_hbm_frac": alg_bytes / (dense_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
 
     gather_ms = None
-    if world > 1:
-        full, gather_ms = gather_com(hist[..., 0].contiguous(), B * world, world, dev)
+    gather_ok = None
+    if dist_on:
+        com_local = hist[..., 0].contiguous()
+        full, gather_ms = gather_com(com_local, B * world, world, dev)
         assert full.shape[0] == B * world
+        a0, a1 = shard_range(B * world, world, rank)
+        gather_ok = bool(torch.equal(full[a0:a1].to(com_local.device), com_local))
+        assert gather_ok, "all-gather did not reassemble this rank's block in place"
 
     # batches pipelined two-deep on two streams (separate history buffers): consecutive
     # rollouts overlap, so one's memory phases run under the other's FP64 phases — what a
@@ -969,13 +1026,15 @@ def main():
             "cpu_baseline": cpu,
             "com_rmse_vs_ref": com_rmse_ref,
             "allgather_ms": gather_ms,
+            "allgather_backend": dist.get_backend() if dist_on else None,
+            "allgather_ok": gather_ok,
             "pcie_inclusive": pcie,
             "pipelined": pipelined,
             "correlation": corr,
             "plan": plan_rec,
         }
         print(json.dumps(line))
-    if world > 1:
+    if dist_on:
         dist.destroy_process_group()
 
 

@@ -347,6 +347,8 @@ static int herdt_check(const zmpc_plan* P, const zmpc_herdt_params* prm, int64_t
       return fail(ZMPC_EINVAL, "polytope facets must be in [3, 16]");
   if (prm->max_footsteps < 0 || prm->max_footsteps > 8)
     return fail(ZMPC_EINVAL, "max_footsteps must be in [0, 8]");
+  if (prm->max_passes < 0 || prm->max_passes > 100000)
+    return fail(ZMPC_EINVAL, "max_passes must be in [0, 100000] (0: default)");
   if (!(prm->alpha > 0) || !(prm->beta >= 0) || !(prm->gamma > 0))
     return fail(ZMPC_EINVAL, "need alpha > 0, beta >= 0, gamma > 0");
   return ZMPC_OK;

@@ -41,7 +41,7 @@
 
 namespace {
 
-constexpr int HMAXIT = 64;  // active-set pass cap (ZMPC_ST_MAXITER beyond)
+constexpr int HMAXIT = 64;  // default active-set pass cap (zmpc_herdt_params.max_passes)
 
 struct HerdtArgs {
   int N;
@@ -78,10 +78,9 @@ struct HerdtArgs {
   double* ws;            // per-wave slab [waves][N][NF][64]
   int nf;                // doubles per row in the slab
   unsigned long long* cnt;  // plan work counters [4..7] (zmpc_plan_counters), may be null
-  int warm;                 // warm start of the last rows (ZMPC_HERDT_WARM, A/B): 0 = row N−1
-                            // free (round 2), 1 = row N−2 free and row N−1 a copy, 2 = row N−1 a
-                            // copy (default), 3 / 4 = the last 2 / 3 rows unshifted
-  unsigned long long* prof; // diagnostics (ZMPC_HERDT_PROF): clock per phase, summed; null
+  int maxit;                // active-set pass cap per solve (ZMPC_ST_MAXITER beyond)
+  unsigned long long* prof; // diagnostics build only (ZMPC_DIAG, ZMPC_HERDT_PROF): clock per
+                            // phase, summed; null in the product library
 };
 
 // Slab row k (4 doubles, written by sweep 2, read by the forward sweep):
@@ -545,6 +544,7 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
     };
 
     double u0 = 0.0, f0 = 0.0;
+    int fstep = 0;  // this solve's failure bits (pass cap, infeasible swing polytope)
     double fsol[MM > 0 ? MM : 1];
     int it = 0, own = 0;  // own: the passes this lane pair needed (diagnostics, ZMPC_HERDT_PROF)
     bool pair_done = false;
@@ -616,7 +616,7 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
           const double fcx = __shfl(fc, lane & ~1, 64), fcy = __shfl(fc, lane | 1, 64);
           double dx, dy;
           if (!polytope_qp(pl, side, nfac, sx, sy, ux - fcx, uy - fcy, &dx, &dy))
-            fq |= ZMPC_ST_INFEASIBLE;
+            fstep |= ZMPC_ST_INFEASIBLE;
           fx0 = axis ? fcy + dy : fcx + dx;
         }
         // the other footsteps minimise V_0 with f0 fixed: the KKT point of F f − g = μ e₀ is
@@ -826,8 +826,8 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
         n_m += (unsigned)m;
         n_m2 += (unsigned)(m * m);
       }
-      if (changed && it >= HMAXIT) {
-        fq |= ZMPC_ST_MAXITER;
+      if (changed && it >= a.maxit) {
+        fstep |= ZMPC_ST_MAXITER;
         changed = false;
       }
       // the pair runs its passes together (the polytope solve reads both lanes)
@@ -835,6 +835,14 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
     }
     if (valid) itmax = max(itmax, (unsigned)it);
     if (valid) pr_own += (unsigned long long)own;
+    // a failed joint QP (either lane of the pair) takes the reference's fallback
+    // (zmp_controller.py:796-802): zero jerk on both axes and the first footstep at the air
+    // foot's centre; the walk's status keeps the failure bit
+    fq |= fstep;
+    if ((fstep | __shfl_xor(fstep, 1, 64)) != 0) {
+      u0 = 0.0;
+      if (m > 0) f0 = air;
+    }
     // ---- advance (reference form x⁺ = A x + B u0, zmp_controller.py:809-810) ----------------
     double xn[3];
     xn[0] = x[0] + T * x[1] + T2 * x[2] + T3 * u0;
@@ -878,14 +886,9 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
     // warm start: the converged set shifted one row towards the present
     // (round 3, config 6: row N−1 a copy of the old last row instead of free — 1.316 → 1.157
     // passes per solve, 86.4 → 78.6 ms; the converged set and the solution do not change)
-    const unsigned char wlast = wset[(N - 1) * 64 + lane];
-    const unsigned char wl2 = N >= 2 ? wset[(N - 2) * 64 + lane] : 0;
-    const unsigned char wl3 = N >= 3 ? wset[(N - 3) * 64 + lane] : 0;
+    // (row N−1 keeps its value; freeing row N−2 as the strict kernel does changed nothing here,
+    // 1.316 passes either way, and keeping the last 2–3 rows unshifted equals the copy)
     for (int k = 0; k < N - 1; ++k) wset[k * 64 + lane] = wset[(k + 1) * 64 + lane];
-    wset[(N - 1) * 64 + lane] = a.warm == 0 ? 0 : wlast;
-    if (a.warm == 1 && N >= 2) wset[(N - 2) * 64 + lane] = 0;
-    if (a.warm >= 3 && N >= 2) wset[(N - 2) * 64 + lane] = wl2;
-    if (a.warm >= 4 && N >= 3) wset[(N - 3) * 64 + lane] = wl3;
   }
   if (valid && a.status != nullptr) {
     const int other = __shfl(fq, lane ^ 1, 64);
@@ -972,7 +975,8 @@ hipError_t zmpc_launch_herdt(const zmpc_plan* p, const zmpc_herdt_params* prm, i
   a.foot = foot;
   a.status = status;
   a.cnt = p->lqcnt;
-  static unsigned long long* prof = [] {  // diagnostics only: per-phase clocks to stderr
+#ifdef ZMPC_DIAG
+  static unsigned long long* prof = [] {  // diagnostics build: per-phase clocks to stderr
     unsigned long long* q = nullptr;
     if (getenv("ZMPC_HERDT_PROF") && hipMalloc((void**)&q, 8 * sizeof(unsigned long long)) != hipSuccess)
       q = nullptr;
@@ -980,11 +984,10 @@ hipError_t zmpc_launch_herdt(const zmpc_plan* p, const zmpc_herdt_params* prm, i
   }();
   if (prof) (void)hipMemsetAsync(prof, 0, 8 * sizeof(unsigned long long), s);
   a.prof = prof;
-  static const int warm = [] {
-    const char* e = getenv("ZMPC_HERDT_WARM");
-    return e ? atoi(e) : 2;
-  }();
-  a.warm = warm;
+#else
+  a.prof = nullptr;
+#endif
+  a.maxit = prm->max_passes > 0 ? prm->max_passes : HMAXIT;
   const int mm = prm->max_footsteps;
   const int MM = mm <= 2 ? 2 : mm <= 4 ? 4 : mm <= 6 ? 6 : mm <= 7 ? 7 : mm <= 8 ? 8 : 0;
   if (MM == 0) {

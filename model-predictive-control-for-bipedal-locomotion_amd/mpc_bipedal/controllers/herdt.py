@@ -111,7 +111,7 @@ class HerdtParams(ctypes.Structure):
                 ("foot_width", ctypes.c_double), ("foot_spread", ctypes.c_double),
                 ("nfacets", ctypes.c_int32 * 2),
                 ("facets", ((ctypes.c_double * 3) * _native.HERDT_MAX_FACETS) * 2),
-                ("max_footsteps", ctypes.c_int32)]
+                ("max_footsteps", ctypes.c_int32), ("max_passes", ctypes.c_int32)]
 
 
 def make_params(config, max_steps: int) -> HerdtParams:

@@ -28,6 +28,7 @@ from . import herdt
 
 _FAILED = "QP solver did not find a solution (infeasible or other)."
 _ST_MAXITER = 1  # include/zmpc.h ZMPC_ST_MAXITER
+_ST_INFEASIBLE = 8  # include/zmpc.h ZMPC_ST_INFEASIBLE
 
 
 class ZMPController:
@@ -53,18 +54,21 @@ class ZMPController:
             raise RuntimeError(_FAILED)
 
     def _herdt_status(self, status):
-        """Herdt drop-ins: the reference never raises on a failed joint QP — it prints a message
-        and continues (zmp_controller.py:796-802).  A walk that reached the active-set pass cap
-        (ZMPC_ST_MAXITER) therefore warns and keeps the kernel's last iterate (the reference
-        would substitute zero jerk and the air foot); any other flag (non-finite, factor,
-        infeasible polytope) raises RuntimeError."""
+        """Herdt drop-ins: the reference never raises on a failed joint QP — it prints a message,
+        substitutes zero jerk and the air foot's centre and continues (zmp_controller.py:796-802).
+        The kernel applies that same fallback to a solve that reached the active-set pass cap
+        (ZMPC_ST_MAXITER) or whose swing polytope is infeasible (ZMPC_ST_INFEASIBLE), so those
+        print the reference's message (and warn); any other flag (non-finite state, footstep
+        factorisation, more footsteps than the kernel was built for) raises RuntimeError."""
         st = status.cpu().numpy() if isinstance(status, torch.Tensor) else np.asarray(status)
-        if st.size and np.any(st & ~_ST_MAXITER):
+        soft = _ST_MAXITER | _ST_INFEASIBLE
+        if st.size and np.any(st & ~soft):
             raise RuntimeError(_FAILED)
-        if st.size and np.any(st & _ST_MAXITER):
-            msg = (f"Joint QP solver failed: active-set pass cap reached in "
-                   f"{int(np.count_nonzero(st & _ST_MAXITER))} walk(s); continuing with the last "
-                   f"iterate")
+        if st.size and np.any(st & soft):
+            msg = (f"Joint QP solver failed in {int(np.count_nonzero(st & soft))} walk(s) "
+                   f"(pass cap: {int(np.count_nonzero(st & _ST_MAXITER))}, infeasible swing "
+                   f"polytope: {int(np.count_nonzero(st & _ST_INFEASIBLE))}); zero jerk and the "
+                   f"air foot's centre were used for those solves")
             print(msg)
             warnings.warn(msg, RuntimeWarning, stacklevel=3)
 
@@ -161,8 +165,10 @@ class ZMPController:
     def predict_herdt_joint(self, x_init, y_init, v_ref, x_fc, y_fc, current_state, state_ref,
                             nb_steps, nb_steps_to_next_state, x_airc, y_airc, foot_side, idx):
         """One joint x/y step (zmp_controller.py:533-826): (next x state (3,1), next y state
-        (3,1), first planned x footstep or None, first planned y footstep or None).  The
-        solver is exact, so the reference's fallback to the air foot (:796-802) never runs."""
+        (3,1), first planned x footstep or None, first planned y footstep or None).  A solve that
+        fails (active-set pass cap, infeasible swing polytope) takes the reference's fallback
+        (:796-802): zero jerk (the kernel) and the air foot's centre x_airc / y_airc as the first
+        footstep (here; the C-ABI step knows only the current foot)."""
         plan = self._plan(nb_steps)
         v = np.asarray(v_ref, np.float64).reshape(1, nb_steps, 2)
         win = herdt.encode_states(state_ref).reshape(1, nb_steps)
@@ -176,9 +182,13 @@ class ZMPController:
         side = np.array([0 if foot_side == "left" else 1], np.int8)
         xn, step, st = plan.herdt_step(prm, x, v, win, cur, foot, side)
         self._herdt_status(st)
+        failed = int(st[0]) & (_ST_MAXITER | _ST_INFEASIBLE)
         xn, step = xn[0].cpu().numpy(), step[0].cpu().numpy()
         fx = None if np.isnan(step[0]) else float(step[0])
         fy = None if np.isnan(step[1]) else float(step[1])
+        if failed and fx is not None and x_airc is not None and y_airc is not None:
+            fx = float(np.asarray(x_airc).reshape(-1)[0])
+            fy = float(np.asarray(y_airc).reshape(-1)[0])
         return xn[0].reshape(3, 1), xn[1].reshape(3, 1), fx, fy
 
     def generate_com_trajectory_herdt_batch(self, x_init, v_ref, state_ref, F_ext=None,

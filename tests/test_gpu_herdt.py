@@ -197,3 +197,52 @@ def test_herdt_too_many_footsteps_flags_the_wave():
     prm = H.make_params(c.config, 2)  # too small on purpose
     _, _, st = plan.herdt_rollout(prm, d["v_ref"], states, nb, np.zeros((4, 2, 3)))
     assert np.all(st.cpu().numpy() != 0)
+
+
+def test_herdt_pass_cap_takes_reference_fallback():
+    """zmpc_herdt_params.max_passes = 1 forces the pass cap on every cold solve that needs a
+    second pass: those report ZMPC_ST_MAXITER and take the reference's failure fallback
+    (zmp_controller.py:796-802) — zero jerk on both axes (x_next = A x exactly) and the first
+    footstep at the air foot's centre (the current foot in the C-ABI step); solves that converge
+    in one pass equal the reference-driven golden.  A capped rollout stays finite and flags
+    only the pass cap."""
+    d = golden("herdt_default.npz")
+    c = ZMPController(MPCConfig(method="herdt"))
+    A = c.A
+    capped = 0
+    for k in range(int(d["n_steps_saved"])):
+        g = lambda key: d[f"step{k}_{key}"]
+        N, m = int(g("N")), int(g("m"))
+        plan = c._plan(N)
+        win = H.encode_states(g("win")).reshape(1, N)
+        cur = H.encode_states([int(g("cur"))])
+        prm = H.make_params(c.config, 8)
+        prm.max_passes = 1
+        x = np.stack([g("x").reshape(3), g("y").reshape(3)])[None]
+        foot = np.array([[float(g("fx")), float(g("fy"))]])
+        xn, step, st = plan.herdt_step(prm, x, g("v").reshape(1, N, 2), win, cur, foot,
+                                       np.array([int(g("side"))], np.int8))
+        stv = int(st[0])
+        xn, step = xn[0].cpu().numpy(), step[0].cpu().numpy()
+        assert (stv & ~1) == 0, (k, stv)
+        if stv & 1:
+            capped += 1
+            assert np.abs(xn[0] - A @ x[0, 0]).max() <= 1e-14, k  # zero jerk
+            assert np.abs(xn[1] - A @ x[0, 1]).max() <= 1e-14, k
+            if m > 0:
+                assert step[0] == foot[0, 0] and step[1] == foot[0, 1], k
+        else:
+            sol = g("sol")
+            assert np.abs(xn[0] - (A @ x[0, 0] + c.B[:, 0] * sol[0])).max() <= 1e-9, k
+    assert capped > 0
+    # capped rollout: finite, only the pass-cap bit
+    plan = c._plan()
+    n = len(d["states"])
+    pad = np.concatenate([d["states"], np.repeat(d["states"][-1:], plan.N)])
+    nb = np.array([t[0] for t in H.find_nb_steps(pad)][:n], np.int32)
+    prm = H.make_params(c.config, H.max_footsteps(pad[None], plan.N, n))
+    prm.max_passes = 1
+    hist, foot, st = plan.herdt_rollout(prm, d["v_ref"], d["states"], nb, np.zeros((4, 2, 3)))
+    stv = st.cpu().numpy()
+    assert np.all((stv & ~1) == 0) and np.any(stv & 1)
+    assert bool(torch.isfinite(hist).all()) and bool(torch.isfinite(foot).all())

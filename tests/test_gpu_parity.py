@@ -773,6 +773,58 @@ def test_strict_shared_cop_config4():
     assert np.abs(h[:, :, 0] - h[0:1, :, 0]).max() <= 1e-12
 
 
+def _oracle_strict_walk_b(job):
+    """Spawned worker: oracle.rollout_strict of one per-walk config-3 walk (1 BLAS thread)."""
+    x0, zx, zn, kick, ks, dt = job
+    from threadpoolctl import threadpool_limits
+    with threadpool_limits(1):
+        return O.rollout_strict(x0[0], x0[1], zx, zn, 150, dt, H, G, Q, R, kick=kick,
+                                kick_step=ks)
+
+
+def test_strict_config3_full_size():
+    """BASELINE config 3 at its full per-GPU size: B = 65 536 default.json walks with per-walk
+    rigid offsets (seed 20251226), x0 ~ U(−0.01, 0.01), F_ext ~ U(0, 800) N at
+    n//2, strict (zmp_controller.py:173-195).  Every status is 0; translating CoP and x0 by
+    δ = 0.0625 translates every CoM position by δ; 44 walks spread over the whole launch —
+    lane positions of the first and the last workgroups and one walk of every 8th workgroup
+    in the kernel's kick order (order.hip: walks sorted by (kick step, float32 kick), stable)
+    — equal the oracle's exact rollout at ≤ 1e-9 CoM RMSE."""
+    import multiprocessing
+    from concurrent.futures import ProcessPoolExecutor
+    B = 65536
+    zmax, zmin, x0, F, dt = synthetic_batch(B, 150)
+    n = zmax.shape[1]
+    kick = dt * F / M
+    p = plan(150, strict=True, dt=dt)
+    zx_d = torch.as_tensor(zmax, device="cuda")
+    zn_d = torch.as_tensor(zmin, device="cuda")
+    x0_d = torch.as_tensor(x0, device="cuda")
+    kick_d = torch.as_tensor(kick, device="cuda")
+    h1, s1 = p.rollout(zx_d, zn_d, x0_d, kick=kick_d, kick_step=n // 2)
+    assert int(s1.abs().max()) == 0
+    delta = 0.0625
+    x1 = x0_d.clone()
+    x1[:, :, 0] += delta
+    h2, s2 = p.rollout(zx_d + delta, zn_d + delta, x1, kick=kick_d, kick_step=n // 2)
+    assert int(s2.abs().max()) == 0
+    assert float(((h2 - h1)[..., 0] - delta).abs().max()) <= 1e-7
+    del h2, x1
+    order = np.argsort(kick.astype(np.float32), kind="stable")   # lane position -> walk
+    wg = 256  # lane positions per 8-wave workgroup
+    pos = [0, 1, 63, 64, 127, 200, 255, B - 256, B - 193, B - 64, B - 2, B - 1]
+    pos += [w * wg + (w * 37) % wg for w in range(0, B // wg, 8)]
+    walks = [int(order[q]) for q in pos]
+    h = h1[walks].cpu().numpy()
+    jobs = [(x0[b], zmax[b], zmin[b], float(kick[b]), n // 2, dt) for b in walks]
+    with ProcessPoolExecutor(max_workers=16,
+                             mp_context=multiprocessing.get_context("spawn")) as ex:
+        refs = list(ex.map(_oracle_strict_walk_b, jobs))
+    for i, (b, ref) in enumerate(zip(walks, refs)):
+        assert rmse(h[i, :, :, 0], ref[:, :, 0]) <= 1e-9, b
+        assert np.abs(h[i] - ref).max() <= 1e-6, b
+
+
 def test_strict_shared_cop_full_size_properties():
     """Config 4 at its full per-GPU size (125 000 scenarios, shared CoP): every scenario's
     status is 0, the x-axis rows are the same for every scenario, and translating the CoP

@@ -64,11 +64,13 @@ def test_max_footsteps_brute_force():
 
 def test_herdt_params_struct_layout():
     """HerdtParams mirrors zmpc_herdt_params (include/zmpc.h): 6 doubles, int32[2],
-    double[2][16][3], int32 — 832 bytes with the trailing padding."""
-    assert ctypes.sizeof(H.HerdtParams) == 6 * 8 + 2 * 4 + 2 * 16 * 3 * 8 + 8
+    double[2][16][3], int32 max_footsteps, int32 max_passes — 832 bytes."""
+    assert ctypes.sizeof(H.HerdtParams) == 6 * 8 + 2 * 4 + 2 * 16 * 3 * 8 + 4 + 4
+    assert H.HerdtParams.max_passes.offset == 6 * 8 + 2 * 4 + 2 * 16 * 3 * 8 + 4
     p = H.make_params(MPCConfig(), 6)
     assert p.nfacets[0] == len(golden("herdt_default.npz")["poly_left_b"])
     assert p.max_footsteps == 6
+    assert p.max_passes == 0  # the library's default cap
     with pytest.raises(ValueError, match="footsteps"):
         H.make_params(MPCConfig(), 9)
 
