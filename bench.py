@@ -875,7 +875,7 @@ def main():
 
     # the correlation form the rollout took: the sparse-difference form (rollout.hip
     # axis_correlate_sparse) for waves whose axis has ≤ 40 z_ref changes, else dense.  The dense
-    # form is timed on the same inputs beside it (ZMPC_SPARSE_CORR=0, read per launch)
+    # form is timed on the same inputs beside it (plan option ZMPC_OPT_CORRELATION = 1)
     corr = None
     if rank == 0 and not cfg.strict and not wl["shared"] and not args.no_dense_leg:
         zr = (zmax_h + zmin_h) / 2
@@ -883,21 +883,17 @@ def main():
         wide = n - 1 > 512  # wide kernel: its own limit, and a walk is sparse if both axes are
         lim = SPARSE_MAX_WIDE if wide else SPARSE_MAX
         sparse_frac = float((ch.max(axis=1) <= lim).mean() if wide else (ch <= lim).mean())
-        prev = os.environ.get("ZMPC_SPARSE_CORR")
-        os.environ["ZMPC_SPARSE_CORR"] = "0"
+        plan.set_option("correlation", 1)  # ZMPC_OPT_CORRELATION: dense forms only
         try:
             for _ in range(max(1, args.warmup)):
                 launch()
             torch.cuda.synchronize()
             _, dense_ms = timed_region(launch, args.steps, False, dev)
         finally:
-            if prev is None:
-                os.environ.pop("ZMPC_SPARSE_CORR")
-            else:
-                os.environ["ZMPC_SPARSE_CORR"] = prev
+            plan.set_option("correlation", 0)
             launch()  # the history the rest of the run reads comes from the default form
             torch.cuda.synchronize()
-        corr = {"form": "sparse-difference" if prev != "0" else "dense",
+        corr = {"form": "sparse-difference",
                 "sparse_max_changes_per_axis": lim,
                 "zref_changes_per_axis_mean": float(ch.mean()),
                 "zref_changes_per_axis_max": int(ch.max()),

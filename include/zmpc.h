@@ -13,8 +13,11 @@
  *  - Return 0 on success, a negative ZMPC_E* code on failure; zmpc_last_error() returns a
  *    thread-local message for the last failure on the calling thread.  No C++ exception
  *    crosses the ABI.
- *  - A plan is immutable after creation and may be shared across threads and streams of
- *    its device.
+ *  - A plan is immutable after creation (and after its zmpc_plan_set_option calls, which
+ *    belong before it is shared) and may be shared across threads and streams of its device.
+ *  - The library reads no environment variable that changes a result: algorithm choices are
+ *    explicit plan options (zmpc_plan_set_option); diagnostic ablations exist only in the
+ *    separate diagnostics build (make diag → libzmpc_diag.so, -DZMPC_DIAG).
  *  - status[b] (int32, may be NULL) receives ZMPC_OK, or a per-instance failure flag
  *    (ZMPC_ST_*).  The reference raises RuntimeError("QP solver did not find a solution")
  *    for a failed strict solve (zmp_controller.py:193-194); the host layer does the same
@@ -29,7 +32,7 @@
 extern "C" {
 #endif
 
-#define ZMPC_ABI_VERSION 6
+#define ZMPC_ABI_VERSION 7
 
 /* return codes */
 #define ZMPC_OK 0
@@ -115,6 +118,34 @@ int zmpc_plan_counters(const zmpc_plan* plan, uint64_t* dst_host, int32_t count,
  */
 #define ZMPC_PLAN_STAGES 12
 int zmpc_plan_timings(const zmpc_plan* plan, float* dst_host, int32_t count);
+
+/*
+ * Algorithm selection on a plan (since ABI 7).  Every option chooses between forms that compute
+ * the same solution — bitwise for ZMPC_OPT_KICK_ORDER, to rounding for the others (the tests hold
+ * each pair to <= 1e-11 on O(1) states); zmpc_plan_create sets the defaults (value 0 unless
+ * stated).  For cross-checks and A/B timing; the reference has no counterpart.
+ *   ZMPC_OPT_CORRELATION    unconstrained rollouts: 0 = auto (the sparse-difference correlation
+ *                           for walks whose z_ref changes at most 40 (64 for walks of more than
+ *                           513 samples) times per axis), 1 = the dense forms only
+ *   ZMPC_OPT_LONG_WALK      unconstrained walks of more than 513 samples: 0 = auto,
+ *                           1 = direct correlation, 2 = FFT correlation (where the transform
+ *                           fits the workgroup), 3 = the chunked one-wave kernel
+ *   ZMPC_OPT_ROLLOUT_KERNEL unconstrained walks of at most 513 samples: 0 = auto, 1 = the
+ *                           one-wave-per-walk kernel (the cross-check of the split kernels)
+ *   ZMPC_OPT_KICK_ORDER     strict rollouts: 1 = walks mapped to lanes in (kick step, kick)
+ *                           order (default), 0 = input order
+ *   ZMPC_OPT_STRICT_SOLVER  strict plans: 0 = the LQ active-set kernel, 1 = the reduced-
+ *                           Cholesky z-space kernel (cross-check; horizons up to 512)
+ * Returns ZMPC_EINVAL for an unknown option or value.
+ */
+#define ZMPC_OPT_CORRELATION 0
+#define ZMPC_OPT_LONG_WALK 1
+#define ZMPC_OPT_ROLLOUT_KERNEL 2
+#define ZMPC_OPT_KICK_ORDER 3
+#define ZMPC_OPT_STRICT_SOLVER 4
+#define ZMPC_NOPTIONS 5
+int zmpc_plan_set_option(zmpc_plan* plan, int32_t option, int64_t value);
+int zmpc_plan_get_option(const zmpc_plan* plan, int32_t option, int64_t* value);
 
 /*
  * Batched ZMPController.predict_wieber_axis (zmp_controller.py:149-201):

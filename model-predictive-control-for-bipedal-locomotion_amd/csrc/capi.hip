@@ -99,8 +99,19 @@ int zmpc_plan_create(int device, int32_t N, double T, double T2_2, double T3_6, 
     // instead of returning them to the driver every time; anything above is released
     hipMemPool_t pool = nullptr;
     if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess && pool) {
+      // (the only environment variable of the product library; memory retention only)
       const char* env = getenv("ZMPC_POOL_KEEP_MB");
-      uint64_t keep = (uint64_t)(env ? atoll(env) : 4096) << 20;
+      long long mb = 4096;
+      if (env) {
+        char* end = nullptr;
+        const long long v = strtoll(env, &end, 10);
+        if (end != env && *end == '\0' && v >= 0 && v <= (1ll << 22))
+          mb = v;
+        else
+          fprintf(stderr, "libzmpc: ignoring ZMPC_POOL_KEEP_MB=%s (expected 0..%lld MiB)\n",
+                  env, 1ll << 22);
+      }
+      uint64_t keep = (uint64_t)mb << 20;
       (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
     }
     if (device < 64) attrs_done[device] = true;
@@ -109,6 +120,11 @@ int zmpc_plan_create(int device, int32_t N, double T, double T2_2, double T3_6, 
 
   zmpc_plan* P = new zmpc_plan();
   P->device = device;
+  if ((e = hipDeviceGetAttribute(&P->cus, hipDeviceAttributeMultiprocessorCount, device)) !=
+      hipSuccess) {
+    delete P;
+    return hip_fail(e, "hipDeviceGetAttribute");
+  }
   P->N = N;
   P->Kpad = (N + 15) & ~15;
   P->strict = strict ? 1 : 0;
@@ -143,13 +159,7 @@ int zmpc_plan_create(int device, int32_t N, double T, double T2_2, double T3_6, 
     return fail(ZMPC_ENOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
   }
   if (strict) {
-    int cus = 0;
-    if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device)) !=
-        hipSuccess) {
-      free_plan(P);
-      return hip_fail(e, "hipDeviceGetAttribute");
-    }
-    P->strict_slots = 2 * cus;
+    P->strict_slots = 2 * P->cus;
     if ((e = hipMalloc((void**)&P->lqtab, zmpc_strict_lq_table_doubles(N) * sizeof(double))) !=
         hipSuccess) {
       free_plan(P);
@@ -201,7 +211,12 @@ int zmpc_plan_create(int device, int32_t N, double T, double T2_2, double T3_6, 
     free_plan(P);
     return hip_fail(e, "plan info copy");
   }
-  if (info != 0 && getenv("ZMPC_DEBUG_PLAN") == nullptr) {  // (debug: keep it for export)
+#ifdef ZMPC_DIAG
+  const bool keep_failed = getenv("ZMPC_DEBUG_PLAN") != nullptr;  // diagnostics: export it
+#else
+  const bool keep_failed = false;
+#endif
+  if (info != 0 && !keep_failed) {
     free_plan(P);
     return fail(ZMPC_ESTATE, "PuᵀPu + (R/Q)I is not positive definite (pivot " +
                                  std::to_string(info) + ")");
@@ -223,6 +238,27 @@ int zmpc_plan_timings(const zmpc_plan* P, float* dst, int32_t count) {
   g_err.clear();
   if (!P || !dst) return fail(ZMPC_EINVAL, "NULL plan or destination");
   for (int i = 0; i < count && i < ZMPC_PLAN_STAGES; ++i) dst[i] = P->stage_ms[i];
+  return ZMPC_OK;
+}
+
+int zmpc_plan_set_option(zmpc_plan* P, int32_t option, int64_t value) {
+  g_err.clear();
+  if (!P) return fail(ZMPC_EINVAL, "NULL plan");
+  static const int64_t hi[ZMPC_NOPTIONS] = {1, 3, 1, 1, 1};  // largest value of each option
+  if (option < 0 || option >= ZMPC_NOPTIONS) return fail(ZMPC_EINVAL, "unknown option");
+  if (value < 0 || value > hi[option])
+    return fail(ZMPC_EINVAL, "option value out of range (0.." + std::to_string(hi[option]) + ")");
+  if (option == ZMPC_OPT_STRICT_SOLVER && value == 1 && (!P->strict || P->N > 512))
+    return fail(ZMPC_EINVAL, "the reduced-Cholesky strict kernel needs a strict plan, N <= 512");
+  P->opt[option] = (int)value;
+  return ZMPC_OK;
+}
+
+int zmpc_plan_get_option(const zmpc_plan* P, int32_t option, int64_t* value) {
+  g_err.clear();
+  if (!P || !value) return fail(ZMPC_EINVAL, "NULL plan or destination");
+  if (option < 0 || option >= ZMPC_NOPTIONS) return fail(ZMPC_EINVAL, "unknown option");
+  *value = P->opt[option];
   return ZMPC_OK;
 }
 

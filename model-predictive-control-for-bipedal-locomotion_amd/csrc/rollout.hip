@@ -202,8 +202,16 @@ struct RolloutArgs {
   int hN;                 // horizon N (ksum layout)
   int64_t pf_ahead;       // one walk per workgroup: touch walk b + pf_ahead's bounds (the next
                           // dispatch round's) into the caches early; 0 = off
-  int pf_late;            // issue that prefetch after this walk's own loads have landed
 };
+
+// Diagnostic ablation bits (ZMPC_DEBUG_ROLLOUT: 1 no correlation, 2 no scan, 4 no history
+// stores, 8 bounds from row 0) — compiled only into the diagnostics build (make diag,
+// -DZMPC_DIAG); the product library has none of them.
+#ifdef ZMPC_DIAG
+__device__ __forceinline__ int dbgb(const RolloutArgs& a, int bit) { return a.dbg & bit; }
+#else
+__device__ __forceinline__ constexpr int dbgb(const RolloutArgs&, int) { return 0; }
+#endif
 
 // a 16-byte store with the non-temporal hint (streamed past the caches)
 __device__ __forceinline__ void st_nt2(double2* p, double2 v) {
@@ -379,7 +387,7 @@ __device__ __forceinline__ void scan_replay_store(const RolloutArgs& a, int64_t 
   // inclusive Kogge-Stone: T_l += P^d T_{l-d}
   Mat3 Pd = P;
   int r2 = 0;
-  for (int d = 1; d < ((a.dbg & 2) ? 1 : 64); d <<= 1, ++r2) {
+  for (int d = 1; d < (dbgb(a, 2) ? 1 : 64); d <<= 1, ++r2) {
     double u0[3], u1[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
@@ -463,7 +471,7 @@ __device__ __forceinline__ void scan_replay_store(const RolloutArgs& a, int64_t 
       for (int m = mbeg; m < min(mbeg + C, nsteps); ++m) replay_step(m, f0[m], f1[m]);
     }
     __syncthreads();
-    if (!(a.dbg & 4)) {
+    if (!dbgb(a, 4)) {
       const int nd2 = (r1 - r0) * 3;  // double2 items
       const double2* src = reinterpret_cast<const double2*>(stage);
       double2* dst = reinterpret_cast<double2*>(hb + (int64_t)r0 * 6);
@@ -491,7 +499,7 @@ __global__ void __launch_bounds__(64) zmpc_rollout_unc_kernel(RolloutArgs a) {
   double* zr0 = smem + a.kcp;
   double* zr1 = zr0 + a.lzp;
   BoundRegs<PF> r;
-  if (!(a.dbg & 8)) load_bounds<PF>(a, b, lane, r);
+  if (!dbgb(a, 8)) load_bounds<PF>(a, b, lane, r);
   // everything the tail needs is requested up front, behind the bound loads
   const double* xb = a.x0 + b * 6;
   const double xi0[3] = {xb[0], xb[1], xb[2]};
@@ -501,7 +509,7 @@ __global__ void __launch_bounds__(64) zmpc_rollout_unc_kernel(RolloutArgs a) {
   store_zref<CW, PF>(a, r, zr0, zr1, lane);
   __syncthreads();
   double a0[CW], a1[CW];
-  if (!(a.dbg & 1)) {
+  if (!dbgb(a, 1)) {
     correlate<CW>(a, ks, zr0, zr1, lane * CW, a0, a1);
   } else {
 #pragma unroll
@@ -531,41 +539,9 @@ __device__ __forceinline__ void axis_load(const RolloutArgs& a, int64_t b, int t
     const int t = u * 128 + tid;
     // clamped rather than predicated (predicated double2 loads here crash the gfx950 backend
     // of ROCm 7.2 in machine copy propagation); dbg bit 8 turns every load into row 0
-    const int tc = (a.dbg & 8) ? 0 : min(t, a.n - 1);
+    const int tc = dbgb(a, 8) ? 0 : min(t, a.n - 1);
     r.hi[u] = zmx[tc];
     r.lo[u] = zmn[tc];
-  }
-}
-
-// z_ref rows of the walk into zr0/zr1; the last row also to last[2] (for the padding).
-template <int CW>
-__device__ __forceinline__ void axis_stage(const RolloutArgs& a, const AxisBounds<CW>& r,
-                                           double* zr0, double* zr1, double* last, int tid) {
-  using ZL = ZrLayout<CW>;
-#pragma unroll
-  for (int u = 0; u < AxisBounds<CW>::PF2; ++u) {
-    const int t = u * 128 + tid;
-    if (t < a.n) {
-      const double v0 = (r.hi[u].x + r.lo[u].x) / 2, v1 = (r.hi[u].y + r.lo[u].y) / 2;
-      zr0[ZL::idx(t)] = v0;
-      zr1[ZL::idx(t)] = v1;
-      if (t == a.n - 1) {
-        last[0] = v0;
-        last[1] = v1;
-      }
-    }
-  }
-}
-
-// The window padding (zmp_controller.py:81-88): rows n..lz-1 repeat the last row.
-template <int CW>
-__device__ __forceinline__ void axis_pad(const RolloutArgs& a, double* zr0, double* zr1,
-                                         const double* last, int tid) {
-  using ZL = ZrLayout<CW>;
-  const double l0 = last[0], l1 = last[1];
-  for (int t = a.n + tid; t < a.lz; t += 128) {
-    zr0[ZL::idx(t)] = l0;
-    zr1[ZL::idx(t)] = l1;
   }
 }
 
@@ -580,7 +556,7 @@ __device__ __forceinline__ void axis_correlate(const RolloutArgs& a, const doubl
     f[m] = 0.0;
     w[m] = z[ZL::idx(1 + m)];
   }
-  for (int j = 0; j < ((a.dbg & 1) ? 0 : a.kc); j += CW) {
+  for (int j = 0; j < (dbgb(a, 1) ? 0 : a.kc); j += CW) {
 #pragma unroll
     for (int jj = 0; jj < CW; ++jj) {
       const double kj = ks[j + jj];
@@ -621,7 +597,7 @@ __device__ __forceinline__ void axis_correlate_ffa(const RolloutArgs& a,
   for (int i = 0; i < NC; ++i) C[i] = 0.0;
 #pragma unroll
   for (int i = 0; i + 1 < NC; ++i) hr[i] = w[2 * i] + w[2 * i + 1];  // h_{s+2i}
-  const int mloop = (a.dbg & 1) ? 0 : a.kfm;
+  const int mloop = dbgb(a, 1) ? 0 : a.kfm;
   const double* tr = kt;
   for (int m0 = 0; m0 < mloop; m0 += U, tr += 4 * U) {
 #pragma unroll
@@ -707,162 +683,20 @@ __device__ __forceinline__ bool axis_correlate_sparse(const RolloutArgs& a, cons
   return true;
 }
 
-// Scan + replay + coalesced store of walk b's axis `axis` (f in registers); `stage` is the
-// walk's (dead) z_ref area, 2·lzp doubles, shared by both waves.
-template <int CW>
-__device__ __forceinline__ void axis_finish(const RolloutArgs& a, int64_t b, int tid,
-                                            const double* f, double* stage, int stage_rows,
-                                            int* flag) {
-  const int axis = tid >> 6, lane = tid & 63;
-  const int n = a.n, nsteps = n - 1;
-  const double* xb = a.x0 + b * 6 + 3 * axis;
-  const double xi[3] = {xb[0], xb[1], xb[2]};
-  const double kk = (axis == 1 && a.kick != nullptr) ? a.kick[b] : 0.0;
-  const int64_t kick_step = (axis == 1) ? kick_step_of(a, b) : -1;
-  const LipmConsts lc = a.lc;
-  const double kx0 = a.kx[0], kx1 = a.kx[1], kx2 = a.kx[2];
-  const double Bv[3] = {lc.T3_6, lc.T2_2, lc.T};
-  Mat3 Ab;
-  {
-    const double A[9] = {1.0, lc.T, lc.T2_2, 0.0, 1.0, lc.T, 0.0, 0.0, 1.0};
-    const double kx[3] = {kx0, kx1, kx2};
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-      for (int j = 0; j < 3; ++j) Ab.m[3 * i + j] = A[3 * i + j] - Bv[i] * kx[j];
-  }
-  // ---- lane-chunk affine scan ----------------------------------------------------------
-  const int mbeg = lane * CW;
-  double sv[3] = {0.0, 0.0, 0.0};
-#pragma unroll
-  for (int q = 0; q < CW; ++q) {
-    if (mbeg + q < nsteps) {
-      double t[3];
-      matvec3(Ab, sv, t);
-      sv[0] = fma(Bv[0], f[q], t[0]);
-      sv[1] = fma(Bv[1], f[q], t[1]);
-      sv[2] = fma(Bv[2], f[q], t[2]);
-      if (mbeg + q == kick_step) sv[1] -= kk;
-    }
-  }
-  const double* Pp = a.scanP + (CW - 1) * kScanStride;  // (Ā^CW)^(2^r), r = 0..5, from the plan
-  if (lane == 0) {
-    double t[3];
-    Mat3 P;
-#pragma unroll
-    for (int q = 0; q < 9; ++q) P.m[q] = Pp[q];
-    matvec3(P, xi, t);
-    for (int i = 0; i < 3; ++i) sv[i] += t[i];
-  }
-#pragma unroll
-  for (int r2 = 0; r2 < 6; ++r2) {
-    const int d = 1 << r2;
-    if (a.dbg & 2) break;
-    double u[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) u[i] = __shfl_up(sv[i], d, 64);
-    if (lane >= d) {
-      Mat3 Pd;
-#pragma unroll
-      for (int q = 0; q < 9; ++q) Pd.m[q] = Pp[r2 * 9 + q];
-      double t[3];
-      matvec3(Pd, u, t);
-      for (int i = 0; i < 3; ++i) sv[i] += t[i];
-    }
-  }
-  double xs0[3];
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const double p = __shfl_up(sv[i], 1, 64);
-    xs0[i] = (lane == 0) ? xi[i] : p;
-  }
-  // ---- replay (reference form) into the shared staging rows, coalesced copy-out ------
-  const int rows_per_round = stage_rows;
-  double* hb = a.hist + b * (int64_t)n * 6;
-  double x[3];
-  for (int r0 = 0; r0 < n; r0 += rows_per_round) {
-    const int r1 = min(r0 + rows_per_round, n);
-    if (lane == 0 && r0 == 0) {
-      stage[3 * axis + 0] = xi[0];
-      stage[3 * axis + 1] = xi[1];
-      stage[3 * axis + 2] = xi[2];
-    }
-#pragma unroll
-    for (int i = 0; i < 3; ++i) x[i] = xs0[i];
-#pragma unroll
-    for (int q = 0; q < CW; ++q) {
-      const int m = mbeg + q;
-      if (m < nsteps) {
-        const double u = f[q] - (kx0 * x[0] + kx1 * x[1] + kx2 * x[2]);
-        double xn[3];
-        lipm_step(lc, x, u, xn);
-        if (m == kick_step) xn[1] -= kk;
-        const int row = m + 1;
-        if (row >= r0 && row < r1) {
-          double* o = stage + (row - r0) * 6 + 3 * axis;
-          o[0] = xn[0];
-          o[1] = xn[1];
-          o[2] = xn[2];
-        }
-#pragma unroll
-        for (int i = 0; i < 3; ++i) x[i] = xn[i];
-      }
-    }
-    __syncthreads();
-    if (!(a.dbg & 4)) {
-      const int nd2 = (r1 - r0) * 3;
-      const double2* src = reinterpret_cast<const double2*>(stage);
-      double2* dst = reinterpret_cast<double2*>(hb + (int64_t)r0 * 6);
-      for (int e = tid; e < nd2; e += 128) dst[e] = src[e];
-    }
-    __syncthreads();
-  }
-  if (a.status != nullptr) {
-    const bool finite = isfinite(x[0]) && isfinite(x[1]) && isfinite(x[2]);
-    const unsigned long long bad = __ballot(!finite);
-    if (lane == 0) flag[axis] = bad ? ZMPC_ST_NONFINITE : 0;
-    __syncthreads();
-    if (tid == 0) a.status[b] = flag[0] | flag[1];
-  }
-}
-
-// One walk per workgroup at 16 walks per CU (64 VGPRs): the history is staged through the
-// z_ref area, a.srows rows per round, the replay recomputed per round.
-template <int CW>
-__global__ void __launch_bounds__(128, 8) zmpc_rollout_unc_axis_kernel(RolloutArgs a) {
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  __shared__ int flag[2];
-  __shared__ double last[2];
-  const int tid = threadIdx.x, lane = tid & 63, axis = tid >> 6;
-  const int64_t b = blockIdx.x;
-  double* zr0 = smem;
-  double* zr1 = zr0 + a.lzp;
-  {
-    AxisBounds<CW> r;
-    axis_load<CW>(a, b, tid, r);
-    axis_stage<CW>(a, r, zr0, zr1, last, tid);
-  }
-  __syncthreads();
-  axis_pad<CW>(a, zr0, zr1, last, tid);
-  __syncthreads();
-  double f[CW];
-  axis_correlate<CW>(a, a.k, axis ? zr1 : zr0, lane, f);  // k: wave-uniform scalar loads
-  __syncthreads();  // z_ref is dead from here on: the area becomes the history staging
-  axis_finish<CW>(a, b, tid, f, zr0, a.srows, flag);
-}
-
-// Split-axis kernel, one walk per 128-thread workgroup with the fewest serial steps: every
-// global load (bounds, the last sample for the window padding, x0, kick) issued up front,
-// z_ref + padding in one pass, one replay writing the whole walk's history rows into the
-// dead z_ref area (LDS sized for it), and one coalesced copy-out — three barriers per walk.
-// One walk of the split kernel (shared by the one-walk-per-workgroup and the persistent
-// launch).  The tables read on wave-uniform addresses come in as __restrict__ pointers so the
-// compiler keeps them on scalar loads even inside a loop that stores the history.
+// Split-axis kernel, one walk per 128-thread workgroup: wave 0 solves the x axis and wave 1 the
+// y axis (half the registers and twice the waves of the one-wave kernel, for latency hiding);
+// they share the staged z_ref and the history staging rows, so loads and stores stay whole-walk
+// coalesced.  The fewest serial steps: every global load (bounds, the last sample for the window
+// padding, x0, kick) issued up front, z_ref + padding in one pass, one replay writing the whole
+// walk's history rows into the dead z_ref area (LDS sized for it), and one coalesced copy-out —
+// three barriers per walk.  The tables read on wave-uniform addresses come in as __restrict__
+// pointers so the compiler keeps them on scalar loads even inside a loop that stores the history.
+// SHF: shared CoP, f precomputed once per launch (zmpc_shared_f_kernel).
 // PM (the persistent kernel): the walk's global loads and its history copy-out are issued at
 // raised wave priority, so a CU's co-resident walks get their memory traffic out ahead of the
 // others' correlation (config 2: 45.3 → 43.8 µs; the one-walk-per-workgroup grid is not helped).
-template <int CW, bool SHF = false, bool PM = false, int RND = 1, bool DPP = false,
-          bool FFA = false>
+// FFA: odd chunk widths take the two-parallel fast-FIR form of the dense correlation.
+template <int CW, bool SHF, bool PM, bool FFA>
 __device__ __forceinline__ void split_walk(const RolloutArgs& a, int64_t b, double* smem,
                                            int* flag, const double* __restrict__ kg,
                                            const double* __restrict__ scanP,
@@ -896,8 +730,9 @@ __device__ __forceinline__ void split_walk(const RolloutArgs& a, int64_t b, doub
       for (int i = tid; i < ksum_rows(a.hN); i += 128) Ts[i] = a.ksum[i];
     // the bounds of the walk the next dispatch round puts on this slot, one double per 64 B
     // (threads 0..63 z_max, 64..127 z_min; two loads cover n ≤ 512 samples), so that round's
-    // loads hit L2 / Infinity Cache instead of HBM under this round's compute
-    if (!a.pf_late && a.pf_ahead > 0 && b + a.pf_ahead < a.B) {
+    // loads hit L2 / Infinity Cache instead of HBM under this round's compute (issued after the
+    // walk's own loads have landed it gained nothing: 29.9 vs 29.5 µs, profiles/r3pf2/)
+    if (a.pf_ahead > 0 && b + a.pf_ahead < a.B) {
       const double* src = (tid < 64 ? a.zmax : a.zmin) + (b + a.pf_ahead) * a.bstride;
       const int ln = tid & 63, nd = 2 * n;
       pf0 = src[min(ln * 8, nd - 1)];
@@ -921,16 +756,9 @@ __device__ __forceinline__ void split_walk(const RolloutArgs& a, int64_t b, doub
       }
     }
     __syncthreads();
-    if (a.pf_late && a.pf_ahead > 0 && b + a.pf_ahead < a.B) {
-      // (A/B) the same prefetch issued once this walk's own loads have landed
-      const double* src = (tid < 64 ? a.zmax : a.zmin) + (b + a.pf_ahead) * a.bstride;
-      const int ln = tid & 63, nd = 2 * n;
-      pf0 = src[min(ln * 8, nd - 1)];
-      pf1 = src[min(ln * 8 + 512, nd - 1)];
-    }
     // ---- 3. correlation (this wave's axis) -------------------------------------------------
     // sparse z_ref differences (piecewise-constant CoP) first, else the dense forms
-    const bool sparse = a.ksum != nullptr && !(a.dbg & 1) &&
+    const bool sparse = a.ksum != nullptr && !dbgb(a, 1) &&
                         axis_correlate_sparse<CW>(a, axis ? zr1 : zr0, Ts, lane, f);
     if (sparse) {
     } else if constexpr (FFA && (CW & 1))
@@ -943,19 +771,9 @@ __device__ __forceinline__ void split_walk(const RolloutArgs& a, int64_t b, doub
   const int64_t kick_step = (axis == 1) ? kick_step_of(a, b) : -1;
   const LipmConsts lc = a.lc;
   const double kx0 = kxp[0], kx1 = kxp[1], kx2 = kxp[2];
-  const double Bv[3] = {lc.T3_6, lc.T2_2, lc.T};
-  Mat3 Ab;
-  {
-    const double A[9] = {1.0, lc.T, lc.T2_2, 0.0, 1.0, lc.T, 0.0, 0.0, 1.0};
-    const double kx[3] = {kx0, kx1, kx2};
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-      for (int j = 0; j < 3; ++j) Ab.m[3 * i + j] = A[3 * i + j] - Bv[i] * kx[j];
-  }
   const int mbeg = lane * CW;
   double sv[3] = {0.0, 0.0, 0.0};
-  if constexpr (DPP) {
+  {
     // the chunk's end state from a zero start as one sum, Σ_q Ā^(CW−1−q) B f_q (plan columns;
     // 3 FMAs per step instead of the 12 of the recursion), plus the kick's −kk Ā^(CW−1−q) e1.
     // Steps past nsteps count too: only lanes whose chunk holds no output follow such a lane.
@@ -972,18 +790,6 @@ __device__ __forceinline__ void split_walk(const RolloutArgs& a, int64_t b, doub
 #pragma unroll
       for (int i = 0; i < 3; ++i) sv[i] = fma(-kk, ek[i], sv[i]);
     }
-  } else {
-#pragma unroll
-    for (int q = 0; q < CW; ++q) {
-      if (mbeg + q < nsteps) {
-        double t[3];
-        matvec3(Ab, sv, t);
-        sv[0] = fma(Bv[0], f[q], t[0]);
-        sv[1] = fma(Bv[1], f[q], t[1]);
-        sv[2] = fma(Bv[2], f[q], t[2]);
-        if (mbeg + q == kick_step) sv[1] -= kk;
-      }
-    }
   }
   const double* Pp = scanP + (CW - 1) * kScanStride;  // (Ā^CW)^(2^r), r = 0..5, from the plan
   if (lane == 0) {
@@ -994,23 +800,7 @@ __device__ __forceinline__ void split_walk(const RolloutArgs& a, int64_t b, doub
     matvec3(P, xi, t);
     for (int i = 0; i < 3; ++i) sv[i] += t[i];
   }
-  if constexpr (DPP) scan_dpp(sv, lane, Pp, scanP + kScanPowOff + (CW - 1) * 33 * 9);
-#pragma unroll
-  for (int r2 = 0; r2 < 6; ++r2) {
-    const int d = 1 << r2;
-    if (DPP || (a.dbg & 2)) break;
-    double u[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) u[i] = __shfl_up(sv[i], d, 64);
-    if (lane >= d) {
-      Mat3 Pd;
-#pragma unroll
-      for (int q = 0; q < 9; ++q) Pd.m[q] = Pp[r2 * 9 + q];
-      double t[3];
-      matvec3(Pd, u, t);
-      for (int i = 0; i < 3; ++i) sv[i] += t[i];
-    }
-  }
+  if (!dbgb(a, 2)) scan_dpp(sv, lane, Pp, scanP + kScanPowOff + (CW - 1) * 33 * 9);
   double x[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
@@ -1018,79 +808,56 @@ __device__ __forceinline__ void split_walk(const RolloutArgs& a, int64_t b, doub
     x[i] = (lane == 0) ? xi[i] : p;
   }
   // ---- 5. replay (reference form) straight into the staged history ------------------------
-  // RND = 2 (A/B): the rows go out in two rounds of ⌈n/2⌉ through half the LDS (more walks
-  // resident per CU), the cheap replay recomputed per round
   double* stage = smem;
-  const int rows_per_round = (n + RND - 1) / RND;
-  const double xs0[3] = {x[0], x[1], x[2]};
+  if (lane == 0) {
+    stage[3 * axis + 0] = xi[0];
+    stage[3 * axis + 1] = xi[1];
+    stage[3 * axis + 2] = xi[2];
+  }
 #pragma unroll
-  for (int rnd = 0; rnd < RND; ++rnd) {
-    const int r0 = rnd * rows_per_round, r1 = min(n, r0 + rows_per_round);
-    if (RND > 1) {
+  for (int q = 0; q < CW; ++q) {
+    const int m = mbeg + q;
+    if (m < nsteps) {
+      const double u = f[q] - (kx0 * x[0] + kx1 * x[1] + kx2 * x[2]);
+      double xn[3];
+      lipm_step(lc, x, u, xn);
+      if (m == kick_step) xn[1] -= kk;  // force kick (zmp_controller.py:90,105-106)
+      double* o = stage + (m + 1) * 6 + 3 * axis;
+      o[0] = xn[0];
+      o[1] = xn[1];
+      o[2] = xn[2];
 #pragma unroll
-      for (int i = 0; i < 3; ++i) x[i] = xs0[i];
+      for (int i = 0; i < 3; ++i) x[i] = xn[i];
     }
-    if (lane == 0 && r0 == 0) {
-      stage[3 * axis + 0] = xi[0];
-      stage[3 * axis + 1] = xi[1];
-      stage[3 * axis + 2] = xi[2];
+  }
+  if (a.status != nullptr) {
+    const bool finite = isfinite(x[0]) && isfinite(x[1]) && isfinite(x[2]);
+    const unsigned long long bad = __ballot(!finite);
+    if (lane == 0) flag[axis] = bad ? ZMPC_ST_NONFINITE : 0;
+  }
+  __syncthreads();
+  // ---- 6. coalesced copy-out ---------------------------------------------------------------
+  if (!dbgb(a, 4)) {
+    if constexpr (PM) __builtin_amdgcn_s_setprio(3);
+    const double2* src = reinterpret_cast<const double2*>(stage);
+    double2* dst = reinterpret_cast<double2*>(hist + b * (int64_t)n * 6);
+    const int ne = n * 3;
+    // four rows in flight per thread (LDS reads batched ahead of the stores); the history is
+    // written once and never re-read here: non-temporal stores (config 4 unconstrained
+    // 0.547 → 0.497 ms in an A/B on one box; config 2 unchanged)
+    int e = tid;
+    for (; e + 3 * 128 < ne; e += 4 * 128) {
+      const double2 v0 = src[e], v1 = src[e + 128], v2 = src[e + 256], v3 = src[e + 384];
+      st_nt2(&dst[e], v0);
+      st_nt2(&dst[e + 128], v1);
+      st_nt2(&dst[e + 256], v2);
+      st_nt2(&dst[e + 384], v3);
     }
-#pragma unroll
-    for (int q = 0; q < CW; ++q) {
-      const int m = mbeg + q;
-      if (m < nsteps) {
-        const double u = f[q] - (kx0 * x[0] + kx1 * x[1] + kx2 * x[2]);
-        double xn[3];
-        lipm_step(lc, x, u, xn);
-        if (m == kick_step) xn[1] -= kk;
-        if (RND == 1 || (m + 1 >= r0 && m + 1 < r1)) {
-          double* o = stage + (m + 1 - r0) * 6 + 3 * axis;
-          o[0] = xn[0];
-          o[1] = xn[1];
-          o[2] = xn[2];
-        }
-#pragma unroll
-        for (int i = 0; i < 3; ++i) x[i] = xn[i];
-      }
-    }
-    if (rnd == RND - 1 && a.status != nullptr) {
-      const bool finite = isfinite(x[0]) && isfinite(x[1]) && isfinite(x[2]);
-      const unsigned long long bad = __ballot(!finite);
-      if (lane == 0) flag[axis] = bad ? ZMPC_ST_NONFINITE : 0;
-    }
-    __syncthreads();
-    // ---- 6. coalesced copy-out ---------------------------------------------------------------
-    if (!(a.dbg & 4)) {
-      if constexpr (PM) __builtin_amdgcn_s_setprio(3);
-      const double2* src = reinterpret_cast<const double2*>(stage);
-      double2* dst = reinterpret_cast<double2*>(hist + b * (int64_t)n * 6 + (int64_t)r0 * 6);
-      const int ne = (r1 - r0) * 3;
-      // four rows in flight per thread (LDS reads batched ahead of the stores); the history is
-      // written once and never re-read here: non-temporal stores (config 4 unconstrained
-      // 0.547 → 0.497 ms in an A/B on one box; config 2 unchanged)
-      int e = tid;
-      for (; e + 3 * 128 < ne; e += 4 * 128) {
-        const double2 v0 = src[e], v1 = src[e + 128], v2 = src[e + 256], v3 = src[e + 384];
-        st_nt2(&dst[e], v0);
-        st_nt2(&dst[e + 128], v1);
-        st_nt2(&dst[e + 256], v2);
-        st_nt2(&dst[e + 384], v3);
-      }
-      for (; e < ne; e += 128) st_nt2(&dst[e], src[e]);
-      if constexpr (PM) __builtin_amdgcn_s_setprio(0);
-    }
-    if (RND > 1 && rnd + 1 < RND) __syncthreads();  // staging read out before the next round
+    for (; e < ne; e += 128) st_nt2(&dst[e], src[e]);
+    if constexpr (PM) __builtin_amdgcn_s_setprio(0);
   }
   if (a.status != nullptr && tid == 0) a.status[b] = flag[0] | flag[1];
   if (a.dbg < 0) hist[tid] = pf0 + pf1;  // never (dbg ≥ 0): keeps the prefetch loads
-}
-
-
-template <int CW, bool SHF = false>
-__global__ void __launch_bounds__(128, 4) zmpc_rollout_unc_split_kernel(RolloutArgs a) {
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  __shared__ int flag[2];
-  split_walk<CW, SHF>(a, blockIdx.x, smem, flag, a.k, a.scanP, a.kx, a.hist);
 }
 
 // Shared CoP (bounds stride 0, e.g. an F_ext sweep over one walk): z_ref, and so f, is the
@@ -1114,238 +881,29 @@ __global__ void __launch_bounds__(256) zmpc_shared_f_kernel(const double* __rest
   fsh[axis * fstride + i] = acc;
 }
 
-// Persistent form: grid = resident workgroups (occupancy × CUs), walks strided over it — the
-// workgroups drift out of phase after the first walk, so one's history stores overlap
-// another's correlation (config 2: 45 µs vs 50 µs one walk per workgroup).
-template <int CW, bool SHF = false>
+// The persistent split kernel (grid = resident workgroups × CUs, walks strided over it): even
+// chunk widths at 1–3 walks per resident slot (config 2 before the fast-FIR form: 45 vs 49 µs).
+// (The tables come through the argument struct: as __restrict__ arguments they go to SGPRs
+// and the DPP scan's per-lane powers push the kernel into spills.)
+template <int CW>
 __global__ void __launch_bounds__(128, 4)
-    zmpc_rollout_unc_pers_kernel(RolloutArgs a, const double* __restrict__ kg,
-                                 const double* __restrict__ scanP,
-                                 const double* __restrict__ kxp, double* __restrict__ hist) {
+    zmpc_rollout_unc_persd_kernel(RolloutArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   __shared__ int flag[2];
   for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x) {
-    split_walk<CW, SHF, true>(a, b, smem, flag, kg, scanP, kxp, hist);
+    split_walk<CW, false, true, false>(a, b, smem, flag, a.k, a.scanP, a.kx, a.hist);
     __syncthreads();  // staging read out before the next walk's z_ref overwrites it
   }
 }
 
-// The persistent split kernel with the DPP lane scan (scan_dpp): the default for config-2
-// shaped batches (variant 8; variant 15 = zmpc_rollout_unc_pers_kernel, the shuffle scan).
-template <int CW, bool FFA = true>
-__global__ void __launch_bounds__(128, 4)
-    zmpc_rollout_unc_persd_kernel(RolloutArgs a, const double* __restrict__ kg,
-                                  const double* __restrict__ scanP,
-                                  const double* __restrict__ kxp, double* __restrict__ hist) {
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  __shared__ int flag[2];
-  // (the tables through the argument struct: as __restrict__ arguments they go to SGPRs and
-  // the DPP scan's per-lane powers push the kernel into spills)
-  for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x) {
-    split_walk<CW, false, true, 1, true, FFA>(a, b, smem, flag, (FFA && (CW & 1)) ? a.kffa : a.k,
-                                              a.scanP, a.kx, a.hist);
-    __syncthreads();
-  }
-}
-
-// One walk per workgroup with the DPP lane scan (variant 6 and large batches of variant 8;
-// variant 16 = zmpc_rollout_unc_split_kernel, the shuffle scan).
-template <int CW, bool SHF = false, bool FFA = true>
+// One walk per workgroup (the default; odd chunk widths with the fast-FIR dense form), and the
+// shared-CoP form (SHF).
+template <int CW, bool SHF>
 __global__ void __launch_bounds__(128, 4) zmpc_rollout_unc_splitd_kernel(RolloutArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   __shared__ int flag[2];
-  split_walk<CW, SHF, false, 1, true, FFA>(a, blockIdx.x, smem, flag,
-                                           (FFA && (CW & 1)) ? a.kffa : a.k, a.scanP, a.kx,
-                                           a.hist);
-}
-
-// Variant 11 (A/B): the persistent split kernel with the history copied out in two rounds, so
-// a walk needs max(z_ref, half the history) of LDS and 12 walks are resident per CU (84 VGPRs,
-// six waves per SIMD) instead of 8.
-template <int CW>
-__global__ void __launch_bounds__(128, 6)
-    zmpc_rollout_unc_pers2_kernel(RolloutArgs a, const double* __restrict__ kg,
-                                  const double* __restrict__ scanP,
-                                  const double* __restrict__ kxp, double* __restrict__ hist) {
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  __shared__ int flag[2];
-  for (int64_t b = blockIdx.x; b < a.B; b += gridDim.x) {
-    split_walk<CW, false, true, 2>(a, b, smem, flag, kg, scanP, kxp, hist);
-    __syncthreads();
-  }
-}
-
-// Variant 12 (A/B): the same two-round copy-out, one walk per workgroup.
-template <int CW>
-__global__ void __launch_bounds__(128, 6) zmpc_rollout_unc_split2_kernel(RolloutArgs a) {
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  __shared__ int flag[2];
-  split_walk<CW, false, false, 2>(a, blockIdx.x, smem, flag, a.k, a.scanP, a.kx, a.hist);
-}
-
-// ---- independent axes (A/B variants 9, 10) ---------------------------------------------------
-// The two waves of a walk never wait for each other before the end of the walk: each loads only
-// its axis's bounds (8-byte loads; the partner's loads of the same lines hit in L2), stages its
-// own z_ref, correlates, scans, replays into its own LDS rows (3 doubles per timestep, aliasing
-// its z_ref area) and copies them out with 8-byte stores into its half of each 48-byte history
-// row (the partner fills the other half; both halves meet in L2).  One barrier per walk, for the
-// walk's status.  LDS per wave: max(lzp, 3n) doubles.
-template <int CW>
-__device__ __forceinline__ void indep_walk(const RolloutArgs& a, int64_t b, double* smem,
-                                           int* flag, const double* __restrict__ kg,
-                                           const double* __restrict__ scanP,
-                                           const double* __restrict__ kxp,
-                                           double* __restrict__ hist, int region) {
-  using ZL = ZrLayout<CW>;
-  constexpr int PF = CW + 1;  // 64·(CW+1) >= n for a single-pass walk
-  const int tid = threadIdx.x, lane = tid & 63, axis = tid >> 6;
-  const int n = a.n, nsteps = n - 1;
-  double* zr = smem + (size_t)axis * region;
-  const double* xb = a.x0 + b * 6 + 3 * axis;
-  const double xi[3] = {xb[0], xb[1], xb[2]};
-  const double kk = (axis == 1 && a.kick != nullptr) ? a.kick[b] : 0.0;
-  // ---- 1. this axis's bounds → z_ref (zmp_controller.py:184,197) + window padding (:81-88)
-  {
-    const double* zmx = a.zmax + b * a.bstride + axis;
-    const double* zmn = a.zmin + b * a.bstride + axis;
-    double hi[PF], lo[PF];
-#pragma unroll
-    for (int u = 0; u < PF; ++u) {
-      const int tc = min(u * 64 + lane, n - 1);  // clamped (no predicated loads)
-      hi[u] = zmx[2 * tc];
-      lo[u] = zmn[2 * tc];
-    }
-    double last = 0.0;
-#pragma unroll
-    for (int u = 0; u < PF; ++u) {
-      const int t = u * 64 + lane;
-      const double v = (hi[u] + lo[u]) / 2;
-      if (t < n) zr[ZL::idx(t)] = v;
-      if (u == ((n - 1) >> 6)) last = v;
-    }
-    last = __shfl(last, (n - 1) & 63, 64);
-    for (int t = n + lane; t < a.lz; t += 64) zr[ZL::idx(t)] = last;
-  }
-  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): this wave's z_ref writes are in LDS
-  __builtin_amdgcn_wave_barrier();
-  double f[CW];
-  axis_correlate<CW>(a, kg, zr, lane, f);
-  // ---- 2. lane-chunk affine scan (as split_walk) ----------------------------------------------
-  const int64_t kick_step = (axis == 1) ? kick_step_of(a, b) : -1;
-  const LipmConsts lc = a.lc;
-  const double kx0 = kxp[0], kx1 = kxp[1], kx2 = kxp[2];
-  const double Bv[3] = {lc.T3_6, lc.T2_2, lc.T};
-  Mat3 Ab;
-  {
-    const double A[9] = {1.0, lc.T, lc.T2_2, 0.0, 1.0, lc.T, 0.0, 0.0, 1.0};
-    const double kx[3] = {kx0, kx1, kx2};
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-#pragma unroll
-      for (int j = 0; j < 3; ++j) Ab.m[3 * i + j] = A[3 * i + j] - Bv[i] * kx[j];
-  }
-  const int mbeg = lane * CW;
-  double sv[3] = {0.0, 0.0, 0.0};
-#pragma unroll
-  for (int q = 0; q < CW; ++q) {
-    if (mbeg + q < nsteps) {
-      double t[3];
-      matvec3(Ab, sv, t);
-      sv[0] = fma(Bv[0], f[q], t[0]);
-      sv[1] = fma(Bv[1], f[q], t[1]);
-      sv[2] = fma(Bv[2], f[q], t[2]);
-      if (mbeg + q == kick_step) sv[1] -= kk;
-    }
-  }
-  const double* Pp = scanP + (CW - 1) * kScanStride;
-  if (lane == 0) {
-    double t[3];
-    Mat3 P;
-#pragma unroll
-    for (int q = 0; q < 9; ++q) P.m[q] = Pp[q];
-    matvec3(P, xi, t);
-    for (int i = 0; i < 3; ++i) sv[i] += t[i];
-  }
-#pragma unroll
-  for (int r2 = 0; r2 < 6; ++r2) {
-    const int d = 1 << r2;
-    double u[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) u[i] = __shfl_up(sv[i], d, 64);
-    if (lane >= d) {
-      Mat3 Pd;
-#pragma unroll
-      for (int q = 0; q < 9; ++q) Pd.m[q] = Pp[r2 * 9 + q];
-      double t[3];
-      matvec3(Pd, u, t);
-      for (int i = 0; i < 3; ++i) sv[i] += t[i];
-    }
-  }
-  double x[3];
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    const double p = __shfl_up(sv[i], 1, 64);
-    x[i] = (lane == 0) ? xi[i] : p;
-  }
-  // ---- 3. replay (reference form) into this wave's rows (aliasing its dead z_ref) ------------
-  __builtin_amdgcn_s_waitcnt(0xC07F);
-  __builtin_amdgcn_wave_barrier();
-  double* stage = zr;
-  if (lane == 0) {
-    stage[0] = xi[0];
-    stage[1] = xi[1];
-    stage[2] = xi[2];
-  }
-#pragma unroll
-  for (int q = 0; q < CW; ++q) {
-    const int m = mbeg + q;
-    if (m < nsteps) {
-      const double u = f[q] - (kx0 * x[0] + kx1 * x[1] + kx2 * x[2]);
-      double xn[3];
-      lipm_step(lc, x, u, xn);
-      if (m == kick_step) xn[1] -= kk;
-      double* o = stage + (m + 1) * 3;
-      o[0] = xn[0];
-      o[1] = xn[1];
-      o[2] = xn[2];
-#pragma unroll
-      for (int i = 0; i < 3; ++i) x[i] = xn[i];
-    }
-  }
-  const bool finite = isfinite(x[0]) && isfinite(x[1]) && isfinite(x[2]);
-  const unsigned long long bad = __ballot(!finite);
-  __builtin_amdgcn_s_waitcnt(0xC07F);
-  __builtin_amdgcn_wave_barrier();
-  // ---- 4. copy-out: element e = 3·row + c of this axis → hist[b, row, axis, c] ---------------
-  {
-    double* hb = hist + b * (int64_t)n * 6 + 3 * axis;
-    int row = lane / 3, c = lane - 3 * row;  // e = lane, advancing by 64 = 21 rows + 1
-    for (int e = lane; e < 3 * n; e += 64) {
-      hb[row * 6 + c] = stage[e];
-      row += 21;
-      c += 1;
-      if (c == 3) {
-        c = 0;
-        ++row;
-      }
-    }
-  }
-  if (lane == 0) flag[axis] = bad ? ZMPC_ST_NONFINITE : 0;
-}
-
-template <int CW, bool PERS>
-__global__ void __launch_bounds__(128, 4)
-    zmpc_rollout_unc_indep_kernel(RolloutArgs a, const double* __restrict__ kg,
-                                  const double* __restrict__ scanP,
-                                  const double* __restrict__ kxp, double* __restrict__ hist,
-                                  int region) {
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  __shared__ int flag[2];
-  for (int64_t b = blockIdx.x; b < a.B; b += PERS ? gridDim.x : a.B) {
-    indep_walk<CW>(a, b, smem, flag, kg, scanP, kxp, hist, region);
-    __syncthreads();
-    if (a.status != nullptr && threadIdx.x == 0) a.status[b] = flag[0] | flag[1];
-  }
+  split_walk<CW, SHF, false, true>(a, blockIdx.x, smem, flag, (CW & 1) ? a.kffa : a.k, a.scanP,
+                                   a.kx, a.hist);
 }
 
 // ---- FFT correlation (long walks) ------------------------------------------------------------
@@ -1540,7 +1098,7 @@ __device__ __forceinline__ bool wide_correlate_sparse(const RolloutArgs& a, cons
     tot1 += scnt[1][v];
     if (v < w) base += scnt[axis][v];
   }
-  if (tot0 > kSparseMaxWide || tot1 > kSparseMaxWide || (a.dbg & 1)) return false;
+  if (tot0 > kSparseMaxWide || tot1 > kSparseMaxWide || dbgb(a, 1)) return false;
   const unsigned long long lt = (1ull << lane) - 1ull;
   double* la = ld + axis * kSparseMaxWide;
   int* lma = lm + axis * kSparseMaxWide;
@@ -1661,7 +1219,7 @@ __global__ void __launch_bounds__(128 * W, E == 4 ? 6 : 4) zmpc_rollout_unc_wide
       double2 hi[4], lo[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const int tc = (a.dbg & 8) ? 0 : min(t0 + u * NT + tid, n - 1);  // padding = last row
+        const int tc = dbgb(a, 8) ? 0 : min(t0 + u * NT + tid, n - 1);  // padding = last row
         hi[u] = zmx[tc];
         lo[u] = zmn[tc];
       }
@@ -1723,7 +1281,7 @@ __global__ void __launch_bounds__(128 * W, E == 4 ? 6 : 4) zmpc_rollout_unc_wide
 #pragma unroll
   for (int r2 = 0; r2 < 6; ++r2) {
     const int d = 1 << r2;
-    if (a.dbg & 2) break;
+    if (dbgb(a, 2)) break;
     double u[3];
 #pragma unroll
     for (int i = 0; i < 3; ++i) u[i] = __shfl_up(sv[i], d, 64);
@@ -1808,7 +1366,7 @@ __global__ void __launch_bounds__(128 * W, E == 4 ? 6 : 4) zmpc_rollout_unc_wide
       }
     }
     __syncthreads();
-    if (!(a.dbg & 4)) {
+    if (!dbgb(a, 4)) {
       const int nd2 = (r1 - r0) * 3;
       const double2* src = reinterpret_cast<const double2*>(stage);
       double2* dst = reinterpret_cast<double2*>(hb + (int64_t)r0 * 6);
@@ -2070,8 +1628,6 @@ __global__ void __launch_bounds__(256) zmpc_step_unc_kernel(
   }
 }
 
-int g_cus = 0;  // CUs of the device the attributes were set on (grid sizing)
-
 // Any walk length: the chunked kernel (its own CW = 8 geometry).
 void launch_chunk(hipStream_t s, const RolloutArgs& a0, int N) {
   const ChunkGeom g = chunk_geom(N);
@@ -2084,197 +1640,89 @@ void launch_chunk(hipStream_t s, const RolloutArgs& a0, int N) {
                      chunk_lds_bytes(g), s, a, g.lc);
 }
 
-// The wide kernel, with the next-dispatch-round prefetch when the batch takes at most
-// ZMPC_PF_ROUNDS (default 2) rounds of resident workgroups.
+// Resident workgroups per CU of a kernel at an LDS size (a small per-host-thread cache keyed by
+// kernel, block size and LDS; every device of the pool is the same gfx950 part).
+int occupancy(const void* kernel, int threads, size_t lds) {
+  struct Entry {
+    const void* k;
+    size_t lds;
+    int threads, occ;
+  };
+  static thread_local Entry cache[32];
+  static thread_local int used = 0;
+  const int n = used < 32 ? used : 32;
+  for (int i = 0; i < n; ++i)
+    if (cache[i].k == kernel && cache[i].lds == lds && cache[i].threads == threads)
+      return cache[i].occ;
+  int occ = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kernel, threads, lds) != hipSuccess)
+    occ = 0;
+  cache[used++ % 32] = Entry{kernel, lds, threads, occ};
+  return occ;
+}
+
+// The wide kernel, with the next-dispatch-round prefetch when the batch takes at most two
+// rounds of resident workgroups (config 5 at ≈2.7 rounds: 64.4 vs 54.3 µs with it, so off there;
+// profiles/r3pfw/).
 template <int C, int W, int E>
-void launch_wide(hipStream_t s, RolloutArgs q, size_t lds, int64_t B) {
-  static const int pf_rounds = [] {
-    const char* e = getenv("ZMPC_PF_ROUNDS");
-    return e ? atoi(e) : 2;
-  }();
-  static thread_local size_t occ_lds = 0;
-  static thread_local int occ = 0;
-  if (pf_rounds > 1 && occ_lds != lds) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &occ, reinterpret_cast<const void*>(zmpc_rollout_unc_wide_kernel<C, W, E>), 128 * W,
-            lds) != hipSuccess)
-      occ = 0;
-    occ_lds = lds;
-  }
-  const int64_t R = (int64_t)std::max(g_cus, 1) * occ;
-  q.pf_ahead = (pf_rounds > 1 && R > 0 && q.n <= 512 * W && B <= pf_rounds * R) ? R : 0;
+void launch_wide(hipStream_t s, RolloutArgs q, size_t lds, int64_t B, int cus) {
+  const int occ = occupancy(reinterpret_cast<const void*>(zmpc_rollout_unc_wide_kernel<C, W, E>),
+                            128 * W, lds);
+  const int64_t R = (int64_t)std::max(cus, 1) * occ;
+  q.pf_ahead = (R > 0 && q.n <= 512 * W && B <= 2 * R) ? R : 0;
   hipLaunchKernelGGL((zmpc_rollout_unc_wide_kernel<C, W, E>), dim3((unsigned)B), dim3(128 * W),
                      lds, s, q);
 }
 
+// Walks of at most 64·8+1 samples (one correlation pass).  The split kernels (a 128-thread
+// workgroup per walk, one wave per axis) when their LDS fits the default 64 KiB ceiling:
+//   shared CoP (f precomputed): zmpc_rollout_unc_splitd_kernel<CW, true>;
+//   odd CW (fast-FIR dense form): one walk per workgroup, with the next-round prefetch when the
+//     batch takes at most two dispatch rounds (config 2: 29.6 → 26.9 µs, profiles/r3pf/; with
+//     more rounds the touched lines are evicted before use, B = 16384: 92 → 117 µs);
+//   even CW: the persistent kernel at 1–3 walks per resident slot, else one walk per workgroup.
+// Otherwise (very long horizons) or with ZMPC_OPT_ROLLOUT_KERNEL = 1 (the cross-check):
+// zmpc_rollout_unc_kernel, one wave per walk.
 template <int CW>
-void launch_unc(const RolloutGeom& g, size_t lds, hipStream_t s, RolloutArgs a) {
-  // Kernel choice; ZMPC_ROLLOUT_VARIANT overrides it for A/B runs (DESIGN.md §4 has the
-  // config-2 measurements): 8 = split, persistent grid (default); 6 = split, one walk per
-  // workgroup (both with the DPP lane scan; 15 / 16 the same with the shuffle scan); 1 =
-  // split-axis at 16 walks per CU staging through the z_ref area; 2 = one wave per walk;
-  // 9 / 10 independent axes; 11 / 12 two-round copy-out.  All single-pass kernels produce the
-  // same histories to rounding (tests/test_gpu_parity.py).
-  static const int variant = [] {
-    const char* e = getenv("ZMPC_ROLLOUT_VARIANT");
-    return e ? atoi(e) : 8;
-  }();
+void launch_unc(const RolloutGeom& g, size_t lds, hipStream_t s, RolloutArgs a, int cus,
+                bool generic) {
   const size_t lds_axis = lds - (size_t)a.kcp * sizeof(double);  // no staged gain row
   size_t lds_split = std::max<size_t>(lds_axis, 6 * (size_t)a.n * sizeof(double));
-  // the sparse-difference correlation runs in the split-axis kernels (split_walk, one copy-out
-  // round) and stages the plan's suffix sums behind the z_ref areas
-  const bool split_family =
-      a.fsh == nullptr && g.passes == 1 && lds_split <= 64 * 1024 &&
-      (variant == 8 || variant == 6 || variant == 15 || variant == 16 || variant == 17 ||
-       variant == 18 || variant == 19);
-  const size_t lds_ks = lds_axis + (size_t)ksum_rows(a.hN) * sizeof(double);
-  const size_t lds_sparse = std::max(lds_ks, lds_split);
-  // two-round copy-out variants (11 / 12): half the staging rows
-  const size_t lds_h2 = std::max<size_t>(lds_axis, 6 * (size_t)((a.n + 1) / 2) * sizeof(double));
-  const bool rnd2 = a.fsh == nullptr && g.passes == 1 && (variant == 11 || variant == 12);
-  if (split_family && a.ksum != nullptr && lds_sparse <= 64 * 1024)
+  // the sparse-difference correlation stages the plan's suffix sums behind the z_ref areas
+  const size_t lds_sparse = std::max(lds_axis + (size_t)ksum_rows(a.hN) * sizeof(double),
+                                     lds_split);
+  if (a.ksum != nullptr && lds_sparse <= 64 * 1024)
     lds_split = lds_sparse;
-  else if (!(rnd2 && a.ksum != nullptr && std::max(lds_ks, lds_h2) <= 64 * 1024))
+  else
     a.ksum = nullptr;
-  const size_t lds_h = a.ksum != nullptr ? std::max(lds_ks, lds_h2) : lds_h2;
-  RolloutArgs b = a;
   if (a.fsh != nullptr) {
-    // shared CoP, f precomputed: scan (DPP; variant 16: shuffles), replay and the history
-    // stores only
-    const size_t lds_f = 6 * (size_t)a.n * sizeof(double);
-    if (variant == 16)
-      hipLaunchKernelGGL((zmpc_rollout_unc_split_kernel<CW, true>), dim3((unsigned)a.B),
-                         dim3(128), lds_f, s, a);
-    else
-      hipLaunchKernelGGL((zmpc_rollout_unc_splitd_kernel<CW, true>), dim3((unsigned)a.B),
-                         dim3(128), lds_f, s, a);
+    // shared CoP, f precomputed: scan, replay and the history stores only
+    hipLaunchKernelGGL((zmpc_rollout_unc_splitd_kernel<CW, true>), dim3((unsigned)a.B),
+                       dim3(128), 6 * (size_t)a.n * sizeof(double), s, a);
     return;
   }
-  if (g.passes == 1 && variant == 12) {
-    // (A/B) with the next-round prefetch as the default kernel takes it
-    const char* pe = getenv("ZMPC_PREFETCH");
-    const int pm = pe ? atoi(pe) : 1;
-    int occ12 = 0;
-    if (pm != 0 && hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                       &occ12, reinterpret_cast<const void*>(zmpc_rollout_unc_split2_kernel<CW>),
-                       128, lds_h) != hipSuccess)
-      occ12 = 0;
-    const int64_t R12 = (int64_t)std::max(g_cus, 1) * occ12;
-    RolloutArgs c = a;
-    c.pf_ahead = (pm != 0 && a.n <= 512 && R12 > 0 && a.B <= 2 * R12) ? R12 : 0;
-    c.pf_late = pm == 2;
-    hipLaunchKernelGGL(zmpc_rollout_unc_split2_kernel<CW>, dim3((unsigned)a.B), dim3(128), lds_h,
-                       s, c);
+  if (generic || lds_split > 64 * 1024) {
+    hipLaunchKernelGGL(zmpc_rollout_unc_kernel<CW>, dim3((unsigned)a.B), dim3(64), lds, s, a);
     return;
   }
-  if (g.passes == 1 && variant == 11) {
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &per_cu, reinterpret_cast<const void*>(zmpc_rollout_unc_pers2_kernel<CW>), 128,
-            lds_h) != hipSuccess)
-      per_cu = 0;
-    const int64_t grid = (int64_t)std::max(g_cus, 1) * std::max(per_cu, 1);
-    hipLaunchKernelGGL(zmpc_rollout_unc_pers2_kernel<CW>,
-                       dim3((unsigned)std::min<int64_t>(grid, a.B)), dim3(128), lds_h, s, a, a.k,
-                       a.scanP, a.kx, a.hist);
-    return;
-  }
-  if (g.passes == 1 && (variant == 9 || variant == 10)) {
-    // A/B: independent axes (indep_walk), persistent (9) or one walk per workgroup (10)
-    const int region = (int)std::max<int64_t>(a.lzp, 3 * (int64_t)a.n + 1) & ~1;
-    const size_t lds_i = 2 * (size_t)(region + 2) * sizeof(double);
-    int per_cu = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-            &per_cu, reinterpret_cast<const void*>(zmpc_rollout_unc_indep_kernel<CW, true>), 128,
-            lds_i) != hipSuccess)
-      per_cu = 0;
-    const int64_t grid = (int64_t)std::max(g_cus, 1) * std::max(per_cu, 1);
-    if (variant == 9 && grid < a.B)
-      hipLaunchKernelGGL((zmpc_rollout_unc_indep_kernel<CW, true>), dim3((unsigned)grid),
-                         dim3(128), lds_i, s, a, a.k, a.scanP, a.kx, a.hist, region + 2);
-    else
-      hipLaunchKernelGGL((zmpc_rollout_unc_indep_kernel<CW, false>), dim3((unsigned)a.B),
-                         dim3(128), lds_i, s, a, a.k, a.scanP, a.kx, a.hist, region + 2);
-    return;
-  }
-  if (g.passes == 1 &&
-      (variant == 8 || variant == 6 || variant == 15 || variant == 16 || variant == 17 ||
-       variant == 18 || variant == 19) &&
-      lds_split <= 64 * 1024) {
-    // The lane scan on DPP moves (scan_dpp; round 3: one walk per workgroup 47.9 → 43.5 µs at
-    // B = 4096, 94 → 87 µs at B = 8192, persistent 43.9 → 42.9 µs) and, for odd CW, the fast-FIR
-    // correlation (axis_correlate_ffa).  8 (default): odd CW one walk per workgroup with the
-    // fast-FIR form (config 2, one box, three alternations: 41.6 µs vs 43.3 µs for the round-3
-    // default 17 and 44.7 µs for the persistent fast-FIR 19), even CW as 17; 6: one walk per
-    // workgroup; 17: persistent for B ≤ 3 × the resident grid, direct correlation; 18: one walk
-    // per workgroup, direct; 19: 17's grid with the fast-FIR form; 15 / 16: direct correlation
-    // and the round-2 shuffle scan (A/B)
-    const bool dpp = variant != 15 && variant != 16;
-    const bool ffa = (variant == 8 || variant == 6 || variant == 19) && (CW & 1);
-    const bool pers_v = (variant == 8 && !ffa) || variant == 15 || variant == 17 || variant == 19;
-    const void* pk = !dpp ? reinterpret_cast<const void*>(zmpc_rollout_unc_pers_kernel<CW>)
-                     : ffa ? reinterpret_cast<const void*>(zmpc_rollout_unc_persd_kernel<CW>)
-                           : reinterpret_cast<const void*>(zmpc_rollout_unc_persd_kernel<CW, false>);
-    int per_cu = 0;
-    if (pers_v &&
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pk, 128, lds_split) != hipSuccess)
-      per_cu = 0;
-    static const int per_cu_env = [] {
-      const char* e = getenv("ZMPC_PERS_PER_CU");  // A/B only: resident workgroups per CU
-      return e ? atoi(e) : 0;
-    }();
-    if (per_cu_env > 0) per_cu = std::min(per_cu, per_cu_env);
-    const int64_t grid = (int64_t)std::max(g_cus, 1) * per_cu;
+  if ((CW & 1) == 0) {
+    const int per_cu = occupancy(
+        reinterpret_cast<const void*>(zmpc_rollout_unc_persd_kernel<CW>), 128, lds_split);
+    const int64_t grid = (int64_t)std::max(cus, 1) * per_cu;
     // persistent only for a few walks per workgroup: config 2 (2 per workgroup) 45 µs vs
     // 49 µs; at 8 per workgroup (B = 16384) the one-walk grid is faster (156 vs 177 µs)
     if (per_cu > 0 && grid < a.B && a.B <= 3 * grid) {
-      if (dpp && ffa)
-        hipLaunchKernelGGL(zmpc_rollout_unc_persd_kernel<CW>, dim3((unsigned)grid), dim3(128),
-                           lds_split, s, a, a.k, a.scanP, a.kx, a.hist);
-      else if (dpp)
-        hipLaunchKernelGGL((zmpc_rollout_unc_persd_kernel<CW, false>), dim3((unsigned)grid),
-                           dim3(128), lds_split, s, a, a.k, a.scanP, a.kx, a.hist);
-      else
-        hipLaunchKernelGGL(zmpc_rollout_unc_pers_kernel<CW>, dim3((unsigned)grid), dim3(128),
-                           lds_split, s, a, a.k, a.scanP, a.kx, a.hist);
-    } else if (dpp && ffa) {
-      // ZMPC_PREFETCH=0 turns the next-round bound prefetch off (A/B)
-      static const int pf_mode = [] {
-        const char* e = getenv("ZMPC_PREFETCH");
-        return e ? atoi(e) : 1;
-      }();
-      const bool pf_on = pf_mode != 0;
-      static thread_local size_t occ_lds = 0;  // resident workgroups per CU, per LDS size
-      static thread_local int occ = 0;
-      if (pf_on && occ_lds != lds_split) {
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
-                &occ, reinterpret_cast<const void*>(zmpc_rollout_unc_splitd_kernel<CW>), 128,
-                lds_split) != hipSuccess)
-          occ = 0;
-        occ_lds = lds_split;
-      }
-      // only for two dispatch rounds (config 2: 29.6 → 26.9 µs); with more rounds the rounds
-      // drift apart and the touched lines are evicted before use (B = 16384: 92 → 117 µs)
-      RolloutArgs c = a;
-      const int64_t R = (int64_t)std::max(g_cus, 1) * occ;
-      c.pf_ahead = (pf_on && a.n <= 512 && R > 0 && a.B <= 2 * R) ? R : 0;
-      c.pf_late = pf_mode == 2;
-      hipLaunchKernelGGL(zmpc_rollout_unc_splitd_kernel<CW>, dim3((unsigned)a.B), dim3(128),
-                         lds_split, s, c);
-    } else if (dpp) {
-      hipLaunchKernelGGL((zmpc_rollout_unc_splitd_kernel<CW, false, false>), dim3((unsigned)a.B),
-                         dim3(128), lds_split, s, a);
-    } else {
-      hipLaunchKernelGGL(zmpc_rollout_unc_split_kernel<CW>, dim3((unsigned)a.B), dim3(128),
+      hipLaunchKernelGGL(zmpc_rollout_unc_persd_kernel<CW>, dim3((unsigned)grid), dim3(128),
                          lds_split, s, a);
+      return;
     }
-  } else if (g.passes == 1 && variant != 2 && lds_axis <= 64 * 1024) {
-    b.srows = (int)(lds_axis / (6 * sizeof(double)));
-    hipLaunchKernelGGL(zmpc_rollout_unc_axis_kernel<CW>, dim3((unsigned)a.B), dim3(128), lds_axis,
-                       s, b);
-  } else {
-    hipLaunchKernelGGL(zmpc_rollout_unc_kernel<CW>, dim3((unsigned)a.B), dim3(64), lds, s, a);
   }
+  const int occ = occupancy(
+      reinterpret_cast<const void*>(zmpc_rollout_unc_splitd_kernel<CW, false>), 128, lds_split);
+  const int64_t R = (int64_t)std::max(cus, 1) * occ;
+  a.pf_ahead = (R > 0 && a.n <= 512 && a.B <= 2 * R) ? R : 0;
+  hipLaunchKernelGGL((zmpc_rollout_unc_splitd_kernel<CW, false>), dim3((unsigned)a.B),
+                     dim3(128), lds_split, s, a);
 }
 
 }  // namespace
@@ -2296,24 +1744,44 @@ hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, con
   }
   const RolloutGeom g = rollout_geom(p->N, n);
   const size_t lds = lds_bytes(g);
+#ifdef ZMPC_DIAG
   static const int dbg = [] {
-    const char* e = getenv("ZMPC_DEBUG_ROLLOUT");  // diagnostic ablation bits (0 in production)
+    const char* e = getenv("ZMPC_DEBUG_ROLLOUT");  // diagnostics build: ablation bits
     return e ? atoi(e) : 0;
   }();
-  RolloutArgs a{g.kc, g.kcp, g.lz,      g.lzp, (int)n,     B,   p->lc,
-                p->k, p->kx,  zmax,      zmin,  bstride,    x0,  kick,
-                kick_step,    hist, status, p->scanP, dbg, 0, kick_steps, nullptr, 0,
-                nullptr,      nullptr};
+#else
+  constexpr int dbg = 0;
+#endif
+  RolloutArgs a{};
+  a.kc = g.kc;
+  a.kcp = g.kcp;
+  a.lz = g.lz;
+  a.lzp = g.lzp;
+  a.n = (int)n;
+  a.B = B;
+  a.lc = p->lc;
+  a.k = p->k;
+  a.kx = p->kx;
+  a.zmax = zmax;
+  a.zmin = zmin;
+  a.bstride = bstride;
+  a.x0 = x0;
+  a.kick = kick;
+  a.kick_step = kick_step;
+  a.hist = hist;
+  a.status = status;
+  a.scanP = p->scanP;
+  a.dbg = dbg;
+  a.kick_steps = kick_steps;
   a.kffa = p->kffa;
   a.kfm = g.kfm;
-  // ZMPC_SPARSE_CORR=0: dense correlation only (A/B, the equality tests and bench.py's dense
-  // side measurement; read per launch so that one process can time both forms)
-  const char* sc = getenv("ZMPC_SPARSE_CORR");
-  a.ksum = (sc && atoi(sc) == 0) ? nullptr : p->ksum;
+  // ZMPC_OPT_CORRELATION = 1: the dense correlation forms only (cross-checks, and bench.py's
+  // dense-form timing beside the default)
+  a.ksum = p->opt[ZMPC_OPT_CORRELATION] == 1 ? nullptr : p->ksum;
   a.hN = p->N;
+  const int long_form = p->opt[ZMPC_OPT_LONG_WALK];  // 0 auto, 1 direct, 2 FFT, 3 chunk kernel
   WideGeom wg;
-  static const bool no_wide = getenv("ZMPC_ROLLOUT_NO_WIDE") != nullptr;  // A/B: chunk kernel
-  if (g.passes > 1 && (no_wide || !wide_geom(p->N, n, &wg))) {
+  if (g.passes > 1 && (long_form == 3 || !wide_geom(p->N, n, &wg))) {
     launch_chunk(s, a, p->N);  // any length (the whole walk does not fit one pass)
     return hipGetLastError();
   }
@@ -2330,19 +1798,14 @@ hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, con
     // FFT correlation when the transform maps onto the workgroup (E = P/NT points per thread,
     // 4 or 8), fits the default LDS ceiling and costs less than the direct form: measured
     // crossover (n − 1)·N ≥ 9·P·log2 P — N = 150 walks of 1000/2000 samples
-    // are faster direct, N ≥ 200 faster by FFT.  ZMPC_FFT=0/1 forces the direct form / the FFT
-    // wherever it fits (A/B and tests; ZMPC_NO_FFT = ZMPC_FFT=0).
-    static const int fft_mode = [] {
-      if (getenv("ZMPC_NO_FFT") != nullptr) return 0;
-      const char* e = getenv("ZMPC_FFT");
-      return e ? atoi(e) : -1;
-    }();
+    // are faster direct, N ≥ 200 faster by FFT.  ZMPC_OPT_LONG_WALK 1 / 2 forces the direct
+    // form / the FFT wherever it fits.
     int P = kFftPmin;
     while (P < n - 1 + p->N) P *= 2;
     const int NT = 128 * wg.w;
     int E = (P % NT == 0) ? P / NT : 0;
-    if (fft_mode == 0 || (E != 4 && E != 8) || P > kFftPT || (size_t)P * 16 > 64 * 1024) E = 0;
-    if (fft_mode < 0 && (double)(n - 1) * p->N < 9.0 * P * __builtin_ctz((unsigned)P)) E = 0;
+    if (long_form == 1 || (E != 4 && E != 8) || P > kFftPT || (size_t)P * 16 > 64 * 1024) E = 0;
+    if (long_form == 0 && (double)(n - 1) * p->N < 9.0 * P * __builtin_ctz((unsigned)P)) E = 0;
     if (E) {
       q.fft_tw = reinterpret_cast<const double2*>(p->fft_tw);
       q.fft_g = reinterpret_cast<const double2*>(p->fft_g) + (P - kFftPmin);
@@ -2356,14 +1819,14 @@ hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, con
     else
       q.ksum = nullptr;
     switch (wg.w * 16 + wg.cw) {
-#define ZMPC_WCASE(W, C)                          \
-  case W * 16 + C:                                \
-    if (E == 4)                                   \
-      launch_wide<C, W, 4>(s, q, lds_w, B);       \
-    else if (E == 8)                              \
-      launch_wide<C, W, 8>(s, q, lds_w, B);       \
-    else                                          \
-      launch_wide<C, W, 0>(s, q, lds_w, B);       \
+#define ZMPC_WCASE(W, C)                                \
+  case W * 16 + C:                                      \
+    if (E == 4)                                         \
+      launch_wide<C, W, 4>(s, q, lds_w, B, p->cus);     \
+    else if (E == 8)                                    \
+      launch_wide<C, W, 8>(s, q, lds_w, B, p->cus);     \
+    else                                                \
+      launch_wide<C, W, 0>(s, q, lds_w, B, p->cus);     \
     break;
       ZMPC_WCASE(2, 5) ZMPC_WCASE(2, 6) ZMPC_WCASE(2, 7) ZMPC_WCASE(2, 8)
       ZMPC_WCASE(4, 5) ZMPC_WCASE(4, 6) ZMPC_WCASE(4, 7) ZMPC_WCASE(4, 8)
@@ -2374,10 +1837,10 @@ hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, con
     }
     return hipGetLastError();
   }
+  const bool generic = p->opt[ZMPC_OPT_ROLLOUT_KERNEL] == 1;
   // shared CoP (bounds stride 0) with a single-pass geometry: f once per launch
-  static const bool no_shared_f = getenv("ZMPC_NO_SHARED_F") != nullptr;  // A/B only
   double* fsh = nullptr;
-  if (bstride == 0 && !no_shared_f && 6 * (size_t)n * sizeof(double) <= 64 * 1024) {
+  if (bstride == 0 && !generic && 6 * (size_t)n * sizeof(double) <= 64 * 1024) {
     a.fstride = ((64 * g.cw) + 63) & ~63;  // every lane's CW values, padded
     hipError_t e = hipMallocAsync((void**)&fsh, 2 * (size_t)a.fstride * sizeof(double), s);
     if (e != hipSuccess) {
@@ -2389,9 +1852,9 @@ hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, con
     a.fsh = fsh;
   }
   switch (g.cw) {
-#define ZMPC_CW(C)               \
-  case C:                        \
-    launch_unc<C>(g, lds, s, a); \
+#define ZMPC_CW(C)                                   \
+  case C:                                            \
+    launch_unc<C>(g, lds, s, a, p->cus, generic);    \
     break;
     ZMPC_CW(1) ZMPC_CW(2) ZMPC_CW(3) ZMPC_CW(4) ZMPC_CW(5) ZMPC_CW(6) ZMPC_CW(7) ZMPC_CW(8)
 #undef ZMPC_CW
@@ -2415,13 +1878,10 @@ hipError_t zmpc_launch_step_unc(const zmpc_plan* p, int64_t B, const double* x,
   return hipGetLastError();
 }
 
-// The dynamic-LDS ceiling must be raised once per device for > 64 KiB requests (not for the
-// split-axis kernel, whose 8-waves-per-SIMD bound caps its LDS below that).
+// The dynamic-LDS ceiling must be raised once per device for > 64 KiB requests (the split
+// kernels stay within the default 64 KiB).
 hipError_t zmpc_rollout_unc_set_attrs() {
-  int dev = 0;
-  hipError_t e = hipGetDevice(&dev);
-  if (e == hipSuccess)
-    e = hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, dev);
+  hipError_t e = hipSuccess;
 #define ZMPC_ATTR(C)                                                                        \
   if (e == hipSuccess)                                                                      \
     e = hipFuncSetAttribute((const void*)zmpc_rollout_unc_kernel<C>,                       \

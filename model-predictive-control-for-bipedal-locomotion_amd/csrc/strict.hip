@@ -833,8 +833,13 @@ static hipError_t launch_strict(const zmpc_plan* p, StrictArgs a, hipStream_t s,
   }
   // G packed in LDS when it fits beside a factor room for m <= 32 — N <= ~150; the rest of
   // the room then holds the packed factor
-  // (A/B only: measured slower at N = 150 — the factor room it leaves is too small)
+  // (A/B in the diagnostics build only: measured slower at N = 150 — the factor room it
+  // leaves is too small)
+#ifdef ZMPC_DIAG
   static const bool lds_g = getenv("ZMPC_STRICT_LDS_G") != nullptr;
+#else
+  constexpr bool lds_g = false;
+#endif
   const int gsz = ((p->N * (p->N + 1) / 2) + 1) & ~1;
   a.gsz = (lds_g && strict_lds_bytes(a.Np, a.ld, 32 * 33 / 2, gsz) <= budget) ? gsz : 0;
   // packed factor room for min(|A|, |F|) <= N/2 when it fits, else as much as fits
@@ -864,9 +869,13 @@ static hipError_t launch_strict(const zmpc_plan* p, StrictArgs a, hipStream_t s,
     return hipErrorOutOfMemory;
   }
   const size_t lds = strict_lds_bytes(a.Np, a.ld, a.pcap, a.gsz);
+#ifdef ZMPC_DIAG
   static const bool lds_chol = getenv("ZMPC_STRICT_LDS_CHOL") != nullptr;  // A/B only
+  static const bool dbg_on = getenv("ZMPC_DEBUG_STRICT") != nullptr;       // diagnostics only
+#else
+  constexpr bool lds_chol = false, dbg_on = false;
+#endif
   a.lds_chol = lds_chol ? 1 : 0;
-  static const bool dbg_on = getenv("ZMPC_DEBUG_STRICT") != nullptr;  // diagnostics only
   static unsigned long long* dbgbuf = nullptr;
   if (dbg_on && !dbgbuf) (void)hipMalloc((void**)&dbgbuf, 32 * sizeof(unsigned long long));
   if (dbg_on && dbgbuf) {
@@ -907,12 +916,10 @@ static hipError_t launch_strict(const zmpc_plan* p, StrictArgs a, hipStream_t s,
   return e;
 }
 
-// ZMPC_STRICT_VARIANT=chol selects this file's reduced-Cholesky kernel (A/B and cross-checks);
-// the default is the LQ-form kernel of strict_lq.hip.
+// ZMPC_OPT_STRICT_SOLVER = 1 (zmpc_plan_set_option) selects this file's reduced-Cholesky kernel
+// (cross-checks and A/B); the default is the LQ-form kernel of strict_lq.hip.
 static bool use_chol_variant(const zmpc_plan* p) {
-  static const char* v = getenv("ZMPC_STRICT_VARIANT");
-  static const bool chol = v != nullptr && std::string(v) == "chol";
-  return chol || !zmpc_strict_lq_supported(p);
+  return p->opt[ZMPC_OPT_STRICT_SOLVER] == 1 || !zmpc_strict_lq_supported(p);
 }
 
 hipError_t zmpc_launch_rollout_strict(const zmpc_plan* p, int64_t B, int64_t n,

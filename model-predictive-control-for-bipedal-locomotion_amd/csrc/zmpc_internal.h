@@ -34,6 +34,7 @@ struct LipmConsts {
 
 struct zmpc_plan {
   int device = 0;
+  int cus = 0;      // compute units of the plan's device (grid sizing of the launches)
   int N = 0;        // horizon (nb_steps)
   int Kpad = 0;     // N rounded up to a multiple of 16, the zero-padded length of k
   int strict = 0;
@@ -70,6 +71,8 @@ struct zmpc_plan {
   double* fft_g = nullptr;
   // plan-build stage durations (zmpc_plan_timings), milliseconds
   float stage_ms[ZMPC_PLAN_STAGES] = {};
+  // algorithm options (zmpc_plan_set_option), defaults as include/zmpc.h
+  int opt[ZMPC_NOPTIONS] = {0, 0, 0, 1, 0};
 };
 
 // rows of the fast-FIR tap table: m = 0..⌈(N+1)/2⌉−1, plus zero rows for an unrolled loop

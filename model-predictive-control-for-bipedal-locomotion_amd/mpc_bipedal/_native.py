@@ -12,7 +12,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("ZMPC_LIB", os.path.join(_HERE, "libzmpc.so"))
 
-ABI_VERSION = 6  # include/zmpc.h ZMPC_ABI_VERSION this binding is written for
+ABI_VERSION = 7  # include/zmpc.h ZMPC_ABI_VERSION this binding is written for
 NCOUNTERS = 10   # include/zmpc.h ZMPC_NCOUNTERS
 PLAN_STAGES = 12  # include/zmpc.h ZMPC_PLAN_STAGES
 PLAN_STAGE_NAMES = ("prediction", "gram_PuTPu", "cholesky", "gain", "scan", "fft_tables",
@@ -33,6 +33,10 @@ ST_INFEASIBLE = 8
 
 EXPORT_P, EXPORT_PX, EXPORT_M, EXPORT_K, EXPORT_KX, EXPORT_G, EXPORT_L, EXPORT_HZ = range(8)
 
+# zmpc_plan_set_option (include/zmpc.h ZMPC_OPT_*): algorithm selection, same solutions
+OPTIONS = {"correlation": 0, "long_walk": 1, "rollout_kernel": 2, "kick_order": 3,
+           "strict_solver": 4}
+
 # every symbol include/zmpc.h declares, with (restype, argtypes)
 _c_dbl_p = ctypes.c_void_p  # device pointers travel as integers
 SIGNATURES = {
@@ -50,6 +54,9 @@ SIGNATURES = {
                                           ctypes.c_int32, ctypes.c_int32]),
     "zmpc_plan_timings": (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float),
                                          ctypes.c_int32]),
+    "zmpc_plan_set_option": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64]),
+    "zmpc_plan_get_option": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int32,
+                                            ctypes.POINTER(ctypes.c_int64)]),
     "zmpc_step": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, _c_dbl_p, _c_dbl_p, _c_dbl_p,
                                  _c_dbl_p, ctypes.c_void_p, ctypes.c_void_p]),
     "zmpc_rollout": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, _c_dbl_p,

@@ -103,6 +103,22 @@ class Plan:
                 "herdt_footsteps": int(buf[6]), "herdt_footsteps_sq": int(buf[7]),
                 "max_passes_per_solve": int(buf[8]), "herdt_max_passes_per_solve": int(buf[9])}
 
+    def set_option(self, option, value: int) -> "Plan":
+        """zmpc_plan_set_option: choose between forms that compute the same solution (cross-checks
+        and A/B timing).  option: a name of _native.OPTIONS ("correlation", "long_walk",
+        "rollout_kernel", "kick_order", "strict_solver") or its ZMPC_OPT_* number."""
+        opt = _native.OPTIONS[option] if isinstance(option, str) else int(option)
+        rc = _native.load().zmpc_plan_set_option(self._live(), opt, int(value))
+        _native.check(rc, "zmpc_plan_set_option")
+        return self
+
+    def get_option(self, option) -> int:
+        opt = _native.OPTIONS[option] if isinstance(option, str) else int(option)
+        v = ctypes.c_int64()
+        rc = _native.load().zmpc_plan_get_option(self._live(), opt, ctypes.byref(v))
+        _native.check(rc, "zmpc_plan_get_option")
+        return int(v.value)
+
     def timings(self) -> dict:
         """Plan-build stage durations in ms (zmpc_plan_timings; HIP events on the creation
         stream): name → ms, names as _native.PLAN_STAGE_NAMES."""

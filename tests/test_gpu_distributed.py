@@ -70,7 +70,7 @@ def test_two_ranks_device_shards_reassemble(tmp_path, strict):
     assert np.abs(np.load(out) - ref.cpu().numpy()).max() <= 1e-12
 
 
-def _nccl_rank(port, out):
+def _nccl_rank(rank, port, out):
     """World-size-1 RCCL group on cuda:0 (device_id bound, as bench.py:init does): the device
     all-gather, the bench's timed region (barrier + MAX all-reduce on a device tensor) and
     gather_com all run through the nccl backend."""

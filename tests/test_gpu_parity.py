@@ -352,40 +352,21 @@ def test_long_walks_any_length(N, n):
     assert np.abs(hist.cpu().numpy() - ref).max() <= 1e-8
 
 
-_CHUNK_CHILD = r"""
-import sys, numpy as np, torch
-sys.path.insert(0, sys.argv[1])
-from mpc_bipedal.solver import Plan
-d = np.load(sys.argv[2])
-p = Plan(0, int(d["N"]), float(d["dt"]), 0.75, 9.81, 1.0, 1e-6, False)
-h, _ = p.rollout(d["zmax"], d["zmin"], d["x0"], kick=d["kick"], kick_step=int(d["ks"]))
-np.save(sys.argv[3], h.cpu().numpy())
-"""
-
-
-def test_chunk_kernel_equals_wide_kernel(tmp_path):
-    """The chunked kernel (forced with ZMPC_ROLLOUT_NO_WIDE) and the wide kernel agree on
-    walks the wide kernel covers (514 <= n <= 4097)."""
-    import subprocess
-    import sys
+def test_chunk_kernel_equals_wide_kernel():
+    """The chunked kernel (ZMPC_OPT_LONG_WALK = 3) and the wide kernel agree on walks the wide
+    kernel covers (514 <= n <= 4097)."""
     rng = np.random.default_rng(9)
-    outs = []
     for n in (700, 3000):
         ctr = np.cumsum(rng.normal(0, 0.004, (5, n, 2)), 1)
-        inp = tmp_path / f"in{n}.npz"
-        np.savez(inp, N=150, dt=0.01, zmax=ctr + 0.05, zmin=ctr - 0.05,
-                 x0=rng.normal(0, 0.01, (5, 2, 3)), kick=rng.uniform(0, 0.1, 5), ks=n // 2)
+        zmax, zmin = ctr + 0.05, ctr - 0.05
+        x0 = rng.normal(0, 0.01, (5, 2, 3))
+        kick = rng.uniform(0, 0.1, 5)
         res = []
-        for no_wide in (False, True):
-            out = tmp_path / f"h{n}{int(no_wide)}.npy"
-            env = dict(os.environ)
-            if no_wide:
-                env["ZMPC_ROLLOUT_NO_WIDE"] = "1"
-            subprocess.run([sys.executable, "-c", _CHUNK_CHILD, PKG, str(inp), str(out)],
-                           env=env, check=True, timeout=300)
-            res.append(np.load(out))
+        for form in (0, 3):
+            p = plan(150, dt=0.01).set_option("long_walk", form)
+            h, _ = p.rollout(zmax, zmin, x0, kick=kick, kick_step=n // 2)
+            res.append(h.cpu().numpy())
         assert np.abs(res[0] - res[1]).max() <= 1e-12
-        outs.append(res)
 
 
 def test_kick_step_out_of_range_is_no_kick():
@@ -421,39 +402,27 @@ def test_multi_walk_workgroups_vs_oracle(n):
     assert int(st.abs().max()) == 0
 
 
-_VARIANT_CHILD = r"""
-import sys, numpy as np, torch
-sys.path.insert(0, sys.argv[1])
-from mpc_bipedal.solver import Plan
-d = np.load(sys.argv[2])
-p = Plan(0, 150, float(d["dt"]), 0.75, 9.81, 1.0, 1e-6, False)
-h, _ = p.rollout(d["zmax"], d["zmin"], d["x0"], kick=d["kick"], kick_step=int(d["ks"]))
-np.save(sys.argv[3], h.cpu().numpy())
-"""
-
-
-def test_rollout_kernel_variants_agree(tmp_path):
-    """The single-pass kernels (ZMPC_ROLLOUT_VARIANT 8 split persistent — the default, 6 split
-    one walk per workgroup, both with the DPP lane scan, 15 / 16 the same with the shuffle scan,
-    1 split-axis with z_ref-area staging, 2 one wave per walk, 9/10
-    independent axes persistent / one walk per workgroup, 11 / 12 persistent / one walk per workgroup with a two-round
-    copy-out) agree."""
-    import subprocess
-    import sys
-    zmax, zmin, x0, F, dt = synthetic_batch(4133, 150)
-    n = zmax.shape[1]
-    kick = dt * F / M
-    inp = tmp_path / "in.npz"
-    np.savez(inp, zmax=zmax, zmin=zmin, x0=x0, kick=kick, ks=n // 2, dt=dt)
-    outs = []
-    for v in (8, 6, 15, 16, 17, 18, 19, 1, 2, 9, 10, 11, 12):
-        out = tmp_path / f"h{v}.npy"
-        env = dict(os.environ, ZMPC_ROLLOUT_VARIANT=str(v))
-        subprocess.run([sys.executable, "-c", _VARIANT_CHILD, PKG, str(inp), str(out)],
-                       env=env, check=True, timeout=300)
-        outs.append(np.load(out))
-    for o in outs[1:]:
-        assert np.abs(outs[0] - o).max() <= 1e-12
+def test_rollout_kernel_variants_agree():
+    """The default single-pass kernels (split per axis: one walk per workgroup, the fast-FIR or
+    sparse correlation; persistent for even chunk widths) and the cross-check kernel (one wave
+    per walk, direct correlation: ZMPC_OPT_ROLLOUT_KERNEL = 1) agree, at an odd (n = 420: 7)
+    and an even (n = 360: 6) chunk width, with per-walk and shared CoP."""
+    for Nn, n_cut in ((150, None), (150, 360)):
+        zmax, zmin, x0, F, dt = synthetic_batch(4133, Nn)
+        if n_cut:
+            zmax, zmin = zmax[:, :n_cut], zmin[:, :n_cut]
+        n = zmax.shape[1]
+        kick = dt * F / M
+        outs = []
+        for kern in (0, 1):
+            p = plan(Nn, dt=dt).set_option("rollout_kernel", kern)
+            h, st = p.rollout(zmax, zmin, x0, kick=kick, kick_step=n // 2)
+            assert int(st.abs().max()) == 0
+            outs.append(h.cpu().numpy())
+            hs, _ = p.rollout(zmax[0], zmin[0], x0, kick=kick, kick_step=n // 2)  # shared CoP
+            outs.append(hs.cpu().numpy())
+        assert np.abs(outs[0] - outs[2]).max() <= 1e-12
+        assert np.abs(outs[1] - outs[3]).max() <= 1e-12
 
 
 SPARSE_MAX = 40  # rollout.hip kSparseMax: more z_ref changes per axis take the dense form
@@ -476,31 +445,17 @@ def _piecewise_walks(rng, B, n, changes):
     return zmax + 0.05, zmax - 0.05
 
 
-_SPARSE_CHILD = r"""
-import sys, numpy as np, torch
-sys.path.insert(0, sys.argv[1])
-from mpc_bipedal.solver import Plan
-d = np.load(sys.argv[2])
-p = Plan(0, int(d["N"]), float(d["dt"]), 0.75, 9.81, 1.0, 1e-6, False)
-h, st = p.rollout(d["zmax"], d["zmin"], d["x0"], kick=d["kick"], kick_step=int(d["ks"]))
-assert int(st.abs().max()) == 0
-np.save(sys.argv[3], h.cpu().numpy())
-"""
-
-
 @pytest.mark.parametrize("N,n", ((150, 2), (150, 65), (150, 350), (150, 420), (150, 513),
                                  (512, 1431), (150, 1100), (256, 1000), (150, 2500)))
-def test_sparse_correlation_equals_dense(N, n, tmp_path):
+def test_sparse_correlation_equals_dense(N, n):
     """The sparse-difference correlation (rollout.hip axis_correlate_sparse, the default for
-    piecewise-constant CoP bounds) against the dense forms (ZMPC_SPARSE_CORR=0, a subprocess)
+    piecewise-constant CoP bounds) against the dense forms (ZMPC_OPT_CORRELATION = 1)
     and the oracle, on one batch that mixes default.json walks with rigid offsets, random-walk
     bounds (dense: the fallback), and piecewise-constant bounds with SPARSE_MAX − 1, SPARSE_MAX
     and SPARSE_MAX + 1 changes per axis at random samples including m = 0 and m = n − 2, so
     waves on both sides of the switch sit in one launch.  n covers odd and even chunk widths,
     the split kernels (n ≤ 513) and the wide kernel's FFT and direct forms (longer walks, where
     the limit is SPARSE_MAX_WIDE per axis and a walk is sparse only if both axes are)."""
-    import subprocess
-    import sys
     rng = np.random.default_rng(n + N)
     cop = golden("walk_n150.npz")
     dt = 1.5 / N if N != 150 else float(cop["dt"])
@@ -528,23 +483,16 @@ def test_sparse_correlation_equals_dense(N, n, tmp_path):
     x0[:, :, 0] = rng.uniform(-0.01, 0.01, (B, 2))
     kick = rng.uniform(0, 0.2, B)
     ks = max(n // 3, 0)
-    inp = tmp_path / "in.npz"
-    np.savez(inp, zmax=zmax, zmin=zmin, x0=x0, kick=kick, ks=ks, dt=dt, N=N)
     outs = {}
-    for mode in ("1", "0"):
-        out = tmp_path / f"h{mode}.npy"
-        env = dict(os.environ, ZMPC_SPARSE_CORR=mode)
-        subprocess.run([sys.executable, "-c", _SPARSE_CHILD, PKG, str(inp), str(out)], env=env,
-                       check=True, timeout=300)
-        outs[mode] = np.load(out)
+    for mode in ("1", "0"):  # sparse where it applies (default) / dense only
+        p = plan(N, dt=dt).set_option("correlation", 0 if mode == "1" else 1)
+        h, st = p.rollout(zmax, zmin, x0, kick=kick, kick_step=ks)
+        assert int(st.abs().max()) == 0
+        outs[mode] = h.cpu().numpy()
     scale = np.abs(outs["0"]).max(axis=1, keepdims=True) + 1.0
     assert (np.abs(outs["1"] - outs["0"]) / scale).max() <= 1e-12
     ref = O.rollout_gain(zmax, zmin, x0, N, dt, H, G, Q, R, kick, ks)
     assert np.abs(outs["1"] - ref).max() <= 1e-8
-    # the default path in this process is the sparse one too
-    h, _ = plan(N, dt=dt).rollout(zmax, zmin, x0, kick=kick, kick_step=ks)
-    assert np.array_equal(h.cpu().numpy(), outs["1"]) or \
-        os.environ.get("ZMPC_SPARSE_CORR") == "0"
 
 
 def test_full_size_config2_properties():
@@ -658,28 +606,13 @@ def test_strict_translation_invariance_full_batch():
     assert np.abs(d[..., 0] - 0.0625).max() <= 1e-7
 
 
-_ORDER_CHILD = r"""
-import sys, numpy as np, torch
-sys.path.insert(0, sys.argv[1])
-from mpc_bipedal.solver import Plan
-d = np.load(sys.argv[2])
-p = Plan(0, 150, float(d["dt"]), 0.75, 9.81, 1.0, 1e-6, True)
-h, st = p.rollout(d["zmax"], d["zmin"], d["x0"], kick=d["kick"], kick_step=d["ks"])
-c = p.counters()
-np.savez(sys.argv[3], h=h.cpu().numpy(), st=st.cpu().numpy(), wp=c["wave_passes"],
-         ip=c["instance_passes"])
-"""
-
-
 @pytest.mark.parametrize("shared", (False, True))
-def test_strict_kick_order_same_results(tmp_path, shared):
+def test_strict_kick_order_same_results(shared):
     """order.hip: walks with per-walk kicks are mapped to lanes sorted by (kick step, kick).
     The schedule changes, the results do not: the default run and one in input order
-    (ZMPC_STRICT_ORDER=0, a subprocess) give bitwise the same histories — per-walk bounds and
-    the shared CoP, per-walk kick steps, a batch that is not a multiple of 64 — and the sorted
-    run needs no more wave passes for the same instance passes."""
-    import subprocess
-    import sys
+    (ZMPC_OPT_KICK_ORDER = 0) give bitwise the same histories — per-walk bounds and the shared
+    CoP, per-walk kick steps, a batch that is not a multiple of 64 — and the sorted run needs no
+    more wave passes for the same instance passes."""
     B = 1000
     zmax, zmin, x0, F, dt = synthetic_batch(B, 150, seed=21)
     n = zmax.shape[1]
@@ -688,26 +621,22 @@ def test_strict_kick_order_same_results(tmp_path, shared):
     ks = rng.integers(n // 4, 3 * n // 4, B).astype(np.int64)
     if shared:  # one [n, 2] CoP for every walk (bounds stride 0)
         zmax, zmin, x0 = zmax[0], zmin[0], np.zeros_like(x0)
-    inp = tmp_path / "in.npz"
-    np.savez(inp, zmax=zmax, zmin=zmin, x0=x0, kick=dt * F / M, ks=ks, dt=dt)
     outs = []
-    for mode in ("1", "0"):
-        out = tmp_path / f"o{mode}.npz"
-        env = dict(os.environ, ZMPC_STRICT_ORDER=mode)
-        subprocess.run([sys.executable, "-c", _ORDER_CHILD, PKG, str(inp), str(out)], env=env,
-                       check=True, timeout=300)
-        outs.append(np.load(out))
-    srt, inorder = outs
-    assert int(np.abs(srt["st"]).max()) == 0 and int(np.abs(inorder["st"]).max()) == 0
-    assert np.array_equal(srt["h"], inorder["h"])
-    assert int(srt["ip"]) == int(inorder["ip"])
-    assert int(srt["wp"]) <= int(inorder["wp"])
+    for mode in (1, 0):
+        p = plan(150, strict=True, dt=dt).set_option("kick_order", mode)
+        h, st = p.rollout(zmax, zmin, x0, kick=dt * F / M, kick_step=ks)
+        c = p.counters()
+        assert int(st.abs().max()) == 0
+        outs.append((h.cpu().numpy(), c["wave_passes"], c["instance_passes"]))
+    (hs, wps, ips), (hi, wpi, ipi) = outs
+    assert np.array_equal(hs, hi)
+    assert ips == ipi and wps <= wpi
     # one walk of the batch against the oracle (per-walk kick step)
     b = 777
     zb, nb = (zmax, zmin) if shared else (zmax[b], zmin[b])
     ref = O.rollout_strict(x0[b, 0], x0[b, 1], zb, nb, 150, dt, H, G, Q, R,
                            kick=dt * F[b] / M, kick_step=int(ks[b]))
-    assert rmse(srt["h"][b, :, :, 0], ref[:, :, 0]) <= 1e-9
+    assert rmse(hs[b, :, :, 0], ref[:, :, 0]) <= 1e-9
 
 
 def test_strict_work_counters():
@@ -889,79 +818,45 @@ def test_strict_horizon_limit():
         plan(2561, strict=True)
 
 
-_CHOL_CHILD = r"""
-import sys, numpy as np, torch
-sys.path.insert(0, sys.argv[1])
-from mpc_bipedal.solver import Plan
-s = np.load(sys.argv[2]); l = np.load(sys.argv[3])
-def rmse(a, b): return float(np.sqrt(np.mean((np.asarray(a) - np.asarray(b)) ** 2)))
-errs = {}
-for N in (64, 150):
-    zx, zn = s[f"n{N}_zmax"], s[f"n{N}_zmin"]
-    n = len(zx); dt = 1.5 / N
-    p = Plan(0, N, dt, 0.75, 9.81, 1.0, 1e-6, True)
-    for F in (0, 400, 800):
-        h, st = p.rollout(zx, zn, np.zeros((1, 2, 3)), kick=np.array([dt * F / 40.0]),
-                          kick_step=n // 2)
-        assert int(st.abs().max()) == 0
-        errs[f"n{N}_F{F}"] = rmse(h.cpu().numpy()[0][:, :, 0], s[f"n{N}_F{F}_com"])
-    out, st = p.step(s[f"step{N}_x"], s[f"step{N}_zmax"], s[f"step{N}_zmin"])
-    ref = s[f"step{N}_out"]
-    errs[f"step{N}"] = float(np.abs(out.cpu().numpy() - ref).max() / max(1.0, np.abs(ref).max()))
-p = Plan(0, 400, 1.5 / 400, 0.75, 9.81, 1.0, 1e-6, True)
-zx, zn = l["n400_zmax"], l["n400_zmin"]; n = len(zx)
-x0 = np.stack([l["n400_x0"], l["n400_y0"]])[None]
-h, st = p.rollout(zx, zn, x0, kick=np.array([float(l["n400_kick"])]), kick_step=n // 2)
-assert int(st.abs().max()) == 0
-errs["n400"] = rmse(h.cpu().numpy()[0][:, :, 0], l["n400_com"])
-out, st = p.step(l["step400_x"], l["step400_zmax"], l["step400_zmin"])
-ref = l["step400_out"]
-errs["step400"] = float(np.abs(out.cpu().numpy() - ref).max() / max(1.0, np.abs(ref).max()))
-print(errs)
-for k, v in errs.items():
-    assert v <= (1e-7 if k.startswith("step") else 1e-6), (k, v)
-print("CHOL_OK")
-"""
-
-
 def test_strict_cholesky_variant_vs_oracle():
-    """The reduced-Cholesky strict kernel (strict.hip, ZMPC_STRICT_VARIANT=chol — a cross-check
-    of the default LQ kernel) on the N = 64/150 walks and single solves and on the N = 400
-    long-horizon fixtures (its 320 < N <= 512 range)."""
-    import subprocess
-    import sys
-    env = dict(os.environ, ZMPC_STRICT_VARIANT="chol")
-    r = subprocess.run([sys.executable, "-c", _CHOL_CHILD, PKG,
-                        os.path.join(os.path.dirname(__file__), "golden", "strict_ref.npz"),
-                        os.path.join(os.path.dirname(__file__), "golden",
-                                     "strict_long_ref.npz")],
-                       env=env, capture_output=True, text=True, timeout=600)
-    assert r.returncode == 0 and "CHOL_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
-
-
-_DIRECT_CHILD = r"""
-import sys
-import numpy as np
-sys.path.insert(0, sys.argv[1])
-import torch
-from mpc_bipedal.solver import Plan
-d = np.load(sys.argv[2])
-p = Plan(0, int(d["N"]), float(d["dt"]), 0.75, 9.81, 1.0, 1e-6, False)
-h, _ = p.rollout(d["zmax"], d["zmin"], d["x0"], kick=d["kick"], kick_step=int(d["ks"]))
-np.save(sys.argv[3], h.cpu().numpy())
-print("DIRECT_OK")
-"""
+    """The reduced-Cholesky strict kernel (strict.hip, ZMPC_OPT_STRICT_SOLVER = 1 — a cross-check
+    of the default LQ kernel) on the N = 64/150 walks and single solves of the reference-driven
+    fixtures and on the N = 400 long-horizon fixtures (its 320 < N <= 512 range)."""
+    s = golden("strict_ref.npz")
+    lg = golden("strict_long_ref.npz")
+    for N in (64, 150):
+        zx, zn = s[f"n{N}_zmax"], s[f"n{N}_zmin"]
+        n, dt = len(zx), 1.5 / N
+        p = plan(N, strict=True).set_option("strict_solver", 1)
+        for F in (0, 400, 800):
+            h, st = p.rollout(zx, zn, np.zeros((1, 2, 3)), kick=np.array([dt * F / M]),
+                              kick_step=n // 2)
+            assert int(st.abs().max()) == 0
+            assert rmse(h.cpu().numpy()[0][:, :, 0], s[f"n{N}_F{F}_com"]) <= 1e-6, (N, F)
+        out, st = p.step(s[f"step{N}_x"], s[f"step{N}_zmax"], s[f"step{N}_zmin"])
+        ref = s[f"step{N}_out"]
+        assert np.abs(out.cpu().numpy() - ref).max() <= 1e-7 * max(1.0, np.abs(ref).max())
+    p = plan(400, strict=True).set_option("strict_solver", 1)
+    zx, zn = lg["n400_zmax"], lg["n400_zmin"]
+    n = len(zx)
+    x0 = np.stack([lg["n400_x0"], lg["n400_y0"]])[None]
+    h, st = p.rollout(zx, zn, x0, kick=np.array([float(lg["n400_kick"])]), kick_step=n // 2)
+    assert int(st.abs().max()) == 0
+    assert rmse(h.cpu().numpy()[0][:, :, 0], lg["n400_com"]) <= 1e-6
+    out, st = p.step(lg["step400_x"], lg["step400_zmax"], lg["step400_zmin"])
+    ref = lg["step400_out"]
+    assert np.abs(out.cpu().numpy() - ref).max() <= 1e-7 * max(1.0, np.abs(ref).max())
+    with pytest.raises(ValueError, match="reduced-Cholesky"):
+        plan(600, strict=True).set_option("strict_solver", 1)
 
 
 @pytest.mark.parametrize("N,n", ((512, 1431), (150, 1100), (150, 2500), (256, 1000),
                                  (200, 3000)))
-def test_fft_correlation_equals_direct(N, n, tmp_path):
-    """Long walks: the FFT correlation (rollout.hip, wide kernel; forced with ZMPC_FFT=1 in a
-    subprocess) and the direct form (ZMPC_FFT=0, in a subprocess) on the same batch agree to
-    rounding: max |Δ| ≤ 1e-11 on O(1) states (measured ≈1e-14); the automatic choice (this
-    process: FFT where (n − 1)·N ≥ 9·P·log2 P, e.g. N ≥ 200 here) equals one of them exactly."""
-    import subprocess
-    import sys
+def test_fft_correlation_equals_direct(N, n):
+    """Long walks: the FFT correlation (rollout.hip, wide kernel; ZMPC_OPT_LONG_WALK = 2) and the
+    direct form (= 1) on the same batch agree to rounding: max |Δ| ≤ 1e-11 on O(1) states
+    (measured ≈1e-14); the automatic choice (FFT where (n − 1)·N ≥ 9·P·log2 P, e.g. N ≥ 200
+    here) equals one of them exactly."""
     rng = np.random.default_rng(n)
     dt = 1.5 / N if N == 512 else 0.01
     B = 8
@@ -970,22 +865,14 @@ def test_fft_correlation_equals_direct(N, n, tmp_path):
     x0 = np.zeros((B, 2, 3))
     x0[:, :, 0] = rng.uniform(-0.01, 0.01, (B, 2))
     kick = dt * rng.uniform(0, 800, B) / M
-    f = tmp_path / "in.npz"
-    np.savez(f, zmax=zmax, zmin=zmin, x0=x0, kick=kick, N=N, dt=dt, ks=n // 2)
-    p = plan(N, dt=dt)
-    h_auto, _ = p.rollout(zmax, zmin, x0, kick=kick, kick_step=n // 2)
     h = {}
-    for mode in ("1", "0"):
-        out = tmp_path / f"fft{mode}.npy"
-        env = dict(os.environ, ZMPC_FFT=mode)
-        env.pop("ZMPC_NO_FFT", None)
-        r = subprocess.run([sys.executable, "-c", _DIRECT_CHILD, PKG, str(f), str(out)],
-                           env=env, capture_output=True, text=True, timeout=300)
-        assert r.returncode == 0 and "DIRECT_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-2000:]
-        h[mode] = np.load(out)
-    assert np.abs(h["1"] - h["0"]).max() <= 1e-11
-    h_auto = h_auto.cpu().numpy()
-    assert np.array_equal(h_auto, h["1"]) or np.array_equal(h_auto, h["0"])
+    for form in (0, 1, 2):
+        p = plan(N, dt=dt).set_option("long_walk", form)
+        hh, st = p.rollout(zmax, zmin, x0, kick=kick, kick_step=n // 2)
+        assert int(st.abs().max()) == 0
+        h[form] = hh.cpu().numpy()
+    assert np.abs(h[2] - h[1]).max() <= 1e-11
+    assert np.array_equal(h[0], h[2]) or np.array_equal(h[0], h[1])
 
 
 # ------------------------------------------------ plan build at long horizons
@@ -1028,3 +915,46 @@ def test_plan_cache_bounded_and_destroy():
     p.destroy()  # idempotent
     with pytest.raises(RuntimeError, match="destroyed"):
         p.export(_native.EXPORT_K)
+
+
+_ENV_CHILD = r"""
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+import torch
+from mpc_bipedal.solver import Plan
+d = np.load(sys.argv[2])
+out = {}
+for strict in (False, True):
+    p = Plan(0, 150, float(d["dt"]), 0.75, 9.81, 1.0, 1e-6, strict)
+    h, st = p.rollout(d["zmax"], d["zmin"], d["x0"], kick=d["kick"], kick_step=int(d["ks"]))
+    out[f"h{int(strict)}"] = h.cpu().numpy()
+    out[f"s{int(strict)}"] = st.cpu().numpy()
+np.savez(sys.argv[3], **out)
+"""
+
+
+def test_environment_does_not_change_results(tmp_path):
+    """Every environment switch earlier libraries read (diagnostic ablations that changed results
+    while reporting success, A/B kernel variants) set to a non-default value in a subprocess:
+    the product library's unconstrained and strict rollouts are bitwise those of a clean
+    environment (the switches exist only in the diagnostics build)."""
+    import subprocess
+    import sys
+    from test_host import _DIAG_ENV
+    zmax, zmin, x0, F, dt = synthetic_batch(300, 150, seed=31)
+    n = zmax.shape[1]
+    inp = tmp_path / "in.npz"
+    np.savez(inp, zmax=zmax, zmin=zmin, x0=x0, kick=dt * F / M, ks=n // 2, dt=dt)
+    res = []
+    for dirty in (False, True):
+        env = {k: v for k, v in os.environ.items() if not k.startswith("ZMPC_")}
+        if dirty:
+            env.update({k: "7" for k in _DIAG_ENV})
+            env.update(ZMPC_STRICT_LQ="4x3x4", ZMPC_STRICT_VARIANT="chol", ZMPC_FFT="1")
+        out = tmp_path / f"o{int(dirty)}.npz"
+        subprocess.run([sys.executable, "-c", _ENV_CHILD, PKG, str(inp), str(out)], env=env,
+                       check=True, timeout=300)
+        res.append(np.load(out))
+    for k in ("h0", "s0", "h1", "s1"):
+        assert np.array_equal(res[0][k], res[1][k]), k
+    assert int(np.abs(res[0]["s1"]).max()) == 0

@@ -92,7 +92,7 @@ def test_library_loads_and_exports_every_symbol():
     exported = set(re.findall(r" T (zmpc_\w+)", out))
     assert set(_header_symbols()) <= exported
     lib = _native.load()
-    assert lib.zmpc_abi_version() == _native.ABI_VERSION == 6
+    assert lib.zmpc_abi_version() == _native.ABI_VERSION == 7
     assert lib.zmpc_last_error() == b""
 
 
@@ -127,6 +127,34 @@ def test_argument_errors_without_gpu():
     tbuf = (ctypes.c_float * _native.PLAN_STAGES)()
     rc = lib.zmpc_plan_timings(None, tbuf, _native.PLAN_STAGES)
     assert rc == _native.ZMPC_EINVAL and b"NULL" in lib.zmpc_last_error()
+    rc = lib.zmpc_plan_set_option(None, 0, 0)
+    assert rc == _native.ZMPC_EINVAL and b"NULL" in lib.zmpc_last_error()
+
+
+# environment variables that earlier libraries read to select A/B variants or diagnostic
+# ablations (some of which changed results while reporting success)
+_DIAG_ENV = ("ZMPC_DEBUG_LQ", "ZMPC_DEBUG_ROLLOUT", "ZMPC_DEBUG_PLAN", "ZMPC_DEBUG_STRICT",
+             "ZMPC_ROLLOUT_VARIANT", "ZMPC_STRICT_LQ", "ZMPC_STRICT_NT", "ZMPC_STRICT_WARM",
+             "ZMPC_STRICT_LQ_DRIFT", "ZMPC_STRICT_ORDER", "ZMPC_STRICT_VARIANT", "ZMPC_SPARSE_CORR",
+             "ZMPC_FFT", "ZMPC_NO_FFT", "ZMPC_ROLLOUT_NO_WIDE", "ZMPC_NO_SHARED_F",
+             "ZMPC_PREFETCH", "ZMPC_PF_ROUNDS", "ZMPC_PERS_PER_CU", "ZMPC_HERDT_WARM",
+             "ZMPC_HERDT_PROF", "ZMPC_STRICT_LDS_G", "ZMPC_STRICT_LDS_CHOL")
+
+
+def test_product_library_reads_no_result_changing_environment():
+    """The product libzmpc.so contains no diagnostic / variant switch: the only environment
+    variable it names is ZMPC_POOL_KEEP_MB (memory retention of the stream-ordered pool).
+    Algorithm choices are explicit plan options (zmpc_plan_set_option); ablations live in the
+    separate diagnostics build (make diag).  tests/test_gpu_parity.py
+    test_environment_does_not_change_results runs a rollout with every old switch set."""
+    if not os.path.exists(_native.LIB_PATH):
+        pytest.skip("libzmpc.so not built")
+    blob = open(_native.LIB_PATH, "rb").read()
+    names = set(re.findall(rb"ZMPC_[A-Z0-9_]+", blob))
+    assert names <= {b"ZMPC_POOL_KEEP_MB"}, names
+    for v in _DIAG_ENV:
+        assert v.encode() not in blob, v
+    assert b"getenv" in blob  # (the one read above)
 
 
 def test_router_errors():
