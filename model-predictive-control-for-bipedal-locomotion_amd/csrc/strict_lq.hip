@@ -29,7 +29,7 @@
 //
 // Mapping: a lane owns one instance (one walk, one axis) for the whole rollout; a wave holds
 // 64 walks of one axis.  The bounds come in [axis][t][walk] (a staging transpose), so a wave's
-// load of one window slot is 1 KiB contiguous ((z_max, z_min) pairs, 16 B per lane).  Per pass:
+// load of one window slot is 1 KiB contiguous ((z_ref, half-width) pairs, 16 B per lane).  Per pass:
 //   sweep A  backward Riccati over the horizon in segments of S steps, checkpointing (P, s)
 //            at segment boundaries to a per-lane global slab (coalesced [.., 9, 64]);
 //   sweep B  per segment from the front: reload its checkpoint, recompute its S Riccati
@@ -66,7 +66,7 @@ struct LqArgs {
   int64_t n;             // samples per walk (rollout; 1 in window mode)
   int64_t nsteps;        // timesteps (n − 1, or 1)
   int64_t B;             // walks (rollout) or instances (step)
-  // staged bounds, tiled [axis][group of 64 walks][row][64] of (z_max, z_min) pairs: row t of a
+  // staged bounds, tiled [axis][group of 64 walks][row][64] of (z_ref, half-width) pairs: row t of a
   // window slot holds the group's 64 pairs for time t, one 16-byte load per lane (rows past
   // n − 1 repeat the last sample — the window padding of zmp_controller.py:81-88 — so no
   // clamping in the kernel)
@@ -97,16 +97,16 @@ struct Ric {  // value function V(η) = ½ηᵀPη − sᵀη
 };
 
 template <int S>
-struct SegIn {  // a segment's window slots: bounds and working-set flags
-  double hi[S], lo[S];
-  int f[S];
+struct SegIn {  // a segment's window slots: z_ref, half-width of the box, working-set flags
+  double r[S], h[S];
+  int f[S];  // 0 free, +1 at z_max = r + h, −1 at z_min = r − h
 };
 
 template <int S>
 struct SegOut {  // a segment's feedback (v = −K η − kff) and forward outputs, per step
   double K0[S], K1[S], K2[S], kf[S];
   double w[S];  // forward: z_k − r_k at free slots, v_k at pinned slots
-  int nf[S];    // forward: the free slots' primal verdict (0 stays free, 1/2 violated)
+  int nf[S];    // forward: the free slots' primal verdict (0 stays free, ±1 violated)
 };
 
 // 1/Quu: hardware reciprocal + two Newton steps (Quu ≥ ρ + π² > 0, no special cases)
@@ -142,73 +142,43 @@ __device__ __forceinline__ StepCore step_core(const LqArgs& a, const Ric& v, dou
   return c;
 }
 
-// One backward Riccati step, per-lane slot flag f (0 free, 1 at z_max, 2 at z_min): V_{k+1} in
-// v → V_k; outputs the step's law.
-template <bool LEAN>
-__device__ __forceinline__ void ric_step(const LqArgs& a, Ric& v, double hi, double lo, int f,
+// One backward Riccati step, per-lane signed slot flag f (0 free, +1 at z_max, −1 at z_min):
+// V_{k+1} in v → V_k; outputs the step's law.  Branch-free with σ = f as a double and |σ|: the
+// free part (iqa) and the pinned part (ka, kfa, zero at free slots) of the law,
+// K = Qux·iqa + ka and kff = qu·iqa + kfa — exactly Qux/Quu, qu/Quu at a free slot and c̄/π,
+// −t/π at a pinned one (t = r + σh).  D = Quu K − Qux is formed unconditionally and enters only
+// through ka and kfa, which vanish at free slots.
+__device__ __forceinline__ void ric_step(const LqArgs& a, Ric& v, double r, double h, int f,
                                          double& K0, double& K1, double& K2, double& kf) {
-  const double r = (hi + lo) / 2;  // z_ref (zmp_controller.py:184)
   const StepCore c = step_core(a, v, r);
-  const bool act = f != 0;
   const double iq = recip(c.Quu);
-  if constexpr (LEAN) {
-    // Few per-lane selects: the free part (iqa) and the pinned part (ka, kfa, zero at free
-    // slots) of the law, K = Qux·iqa + ka and kff = qu·iqa + kfa — exactly Qux/Quu, qu/Quu at a
-    // free slot and c̄/π, −t/π at a pinned one.  D = Quu K − Qux is formed unconditionally and
-    // enters only through ka and kfa, which vanish at free slots.
-    const double iqa = act ? 0.0 : iq;
-    const double ka01 = act ? a.ipi : 0.0;
-    const double ka2 = act ? a.gipi : 0.0;
-    const double tz = (f == 1) ? hi : ((f == 2) ? lo : 0.0);
-    const double kfa = -tz * a.ipi;
-    K0 = fma(c.ux0, iqa, ka01);
-    K1 = fma(c.ux1, iqa, ka01);
-    K2 = fma(c.ux2, iqa, ka2);
-    kf = fma(-c.w, iqa, kfa);
-    const double D0 = fma(c.Quu, K0, -c.ux0);
-    const double D1 = fma(c.Quu, K1, -c.ux1);
-    const double D2 = fma(c.Quu, K2, -c.ux2);
-    const double P00 = fma(ka01, D0, fma(-c.ux0, K0, 1.0 + v.p00));
-    const double P01 = fma(ka01, D1, fma(-c.ux0, K1, 1.0 + c.m01));
-    const double P02 = fma(ka01, D2, fma(-c.ux0, K2, a.gp + c.m02));
-    const double P11 = fma(ka01, D1, fma(-c.ux1, K1, 1.0 + c.m11));
-    const double P12 = fma(ka01, D2, fma(-c.ux1, K2, a.gp + c.m12));
-    const double P22 = fma(ka2, D2, fma(-c.ux2, K2, a.gp2 + c.m22));
-    v.s0 = fma(-kfa, D0, fma(-K0, c.w, c.nqx0));
-    v.s1 = fma(-kfa, D1, fma(-K1, c.w, c.nqx1));
-    v.s2 = fma(-kfa, D2, fma(-K2, c.w, c.nqx2));
-    v.p00 = P00;
-    v.p01 = P01;
-    v.p02 = P02;
-    v.p11 = P11;
-    v.p12 = P12;
-    v.p22 = P22;
-  } else {
-    // per-field selects (sweep B: the lean form above needs more registers there)
-    const double t = (f == 1) ? hi : lo;
-    K0 = act ? a.ipi : c.ux0 * iq;
-    K1 = act ? a.ipi : c.ux1 * iq;
-    K2 = act ? a.gipi : c.ux2 * iq;
-    kf = act ? -t * a.ipi : -c.w * iq;
-    const double D0 = act ? fma(c.Quu, K0, -c.ux0) : 0.0;
-    const double D1 = act ? fma(c.Quu, K1, -c.ux1) : 0.0;
-    const double D2 = act ? fma(c.Quu, K2, -c.ux2) : 0.0;
-    const double P00 = fma(K0, D0, fma(-c.ux0, K0, 1.0 + v.p00));
-    const double P01 = fma(K0, D1, fma(-c.ux0, K1, 1.0 + c.m01));
-    const double P02 = fma(K0, D2, fma(-c.ux0, K2, a.gp + c.m02));
-    const double P11 = fma(K1, D1, fma(-c.ux1, K1, 1.0 + c.m11));
-    const double P12 = fma(K1, D2, fma(-c.ux1, K2, a.gp + c.m12));
-    const double P22 = fma(K2, D2, fma(-c.ux2, K2, a.gp2 + c.m22));
-    v.s0 = fma(-kf, D0, fma(-K0, c.w, c.nqx0));
-    v.s1 = fma(-kf, D1, fma(-K1, c.w, c.nqx1));
-    v.s2 = fma(-kf, D2, fma(-K2, c.w, c.nqx2));
-    v.p00 = P00;
-    v.p01 = P01;
-    v.p02 = P02;
-    v.p11 = P11;
-    v.p12 = P12;
-    v.p22 = P22;
-  }
+  const double sg = (double)f, ab = fabs(sg);
+  const double iqa = fma(-ab, iq, iq);  // iq at free slots, exactly 0 at pinned ones
+  const double ka01 = ab * a.ipi;
+  const double ka2 = ab * a.gipi;
+  const double kfa = -fma(sg, h, ab * r) * a.ipi;  // −t/π at pinned slots, 0 at free ones
+  K0 = fma(c.ux0, iqa, ka01);
+  K1 = fma(c.ux1, iqa, ka01);
+  K2 = fma(c.ux2, iqa, ka2);
+  kf = fma(-c.w, iqa, kfa);
+  const double D0 = fma(c.Quu, K0, -c.ux0);
+  const double D1 = fma(c.Quu, K1, -c.ux1);
+  const double D2 = fma(c.Quu, K2, -c.ux2);
+  const double P00 = fma(ka01, D0, fma(-c.ux0, K0, 1.0 + v.p00));
+  const double P01 = fma(ka01, D1, fma(-c.ux0, K1, 1.0 + c.m01));
+  const double P02 = fma(ka01, D2, fma(-c.ux0, K2, a.gp + c.m02));
+  const double P11 = fma(ka01, D1, fma(-c.ux1, K1, 1.0 + c.m11));
+  const double P12 = fma(ka01, D2, fma(-c.ux1, K2, a.gp + c.m12));
+  const double P22 = fma(ka2, D2, fma(-c.ux2, K2, a.gp2 + c.m22));
+  v.s0 = fma(-kfa, D0, fma(-K0, c.w, c.nqx0));
+  v.s1 = fma(-kfa, D1, fma(-K1, c.w, c.nqx1));
+  v.s2 = fma(-kfa, D2, fma(-K2, c.w, c.nqx2));
+  v.p00 = P00;
+  v.p01 = P01;
+  v.p02 = P02;
+  v.p11 = P11;
+  v.p12 = P12;
+  v.p22 = P22;
 }
 
 // The same step for a free slot (ric_step with f = 0 and D = 0 folded: identical values up to
@@ -251,17 +221,17 @@ __device__ __forceinline__ void ric_tail(const LqArgs& a, Ric& v, double r, doub
 }
 
 struct Lane {
-  const double2* hl;  // wave's staged (z_max, z_min) rows (uniform)
+  const double2* hl;  // wave's staged (z_ref, half-width) rows (uniform)
   int lane;
 };
 
-// Per-lane working-set flags of the wave's N slots in LDS (0 free, 1 at z_max, 2 at z_min):
-// one byte per slot, [slot][64].
+// Per-lane working-set flags of the wave's N slots in LDS (0 free, +1 at z_max, −1 at z_min):
+// one signed byte per slot, [slot][64].
 struct Flags {
-  unsigned char* p;
+  signed char* p;
   __device__ __forceinline__ int get(int k, int lane) const { return p[k * 64 + lane]; }
   __device__ __forceinline__ void set(int k, int lane, int v) const {
-    p[k * 64 + lane] = (unsigned char)v;
+    p[k * 64 + lane] = (signed char)v;
   }
 };
 
@@ -277,8 +247,8 @@ __device__ __forceinline__ void seg_load(const LqArgs& a, int j, const Lane& L, 
 #pragma unroll
   for (int q = 0; q < S; ++q) {
     const double2 v = hp[q * 64 + L.lane];
-    in.hi[q] = v.x;
-    in.lo[q] = v.y;
+    in.r[q] = v.x;
+    in.h[q] = v.y;
     if (FLAGS) in.f[q] = fl.get(j * S + q, L.lane);
   }
 }
@@ -305,9 +275,9 @@ __device__ __forceinline__ void seg_riccati(const LqArgs& a, int j, Ric& v, cons
       double K0, K1, K2, kf;
       if (FREE) {
         double iq;
-        ric_free(a, v, (in.hi[q] + in.lo[q]) / 2, K0, K1, K2, kf, iq);
+        ric_free(a, v, in.r[q], K0, K1, K2, kf, iq);
       } else {
-        ric_step<!KEEP>(a, v, in.hi[q], in.lo[q], in.f[q], K0, K1, K2, kf);
+        ric_step(a, v, in.r[q], in.h[q], in.f[q], K0, K1, K2, kf);
       }
       if (KEEP) {
         g.K0[q] = K0;
@@ -333,7 +303,7 @@ __device__ __forceinline__ void seg_tail(const LqArgs& a, const double* __restri
     if (FULL || k < a.N) {
       const double* t = tab + (size_t)k * TAB;
       double kf;
-      ric_tail(a, v, (in.hi[q] + in.lo[q]) / 2, t[0], t[1], t[2], t[3], kf);
+      ric_tail(a, v, in.r[q], t[0], t[1], t[2], t[3], kf);
       if (KEEP) g.kf[q] = kf;
     }
   }
@@ -363,10 +333,9 @@ __device__ __forceinline__ void seg_forward(const LqArgs& a, int j, const SegIn<
       double u, z;
       fwd_step(a, g.K0[q], g.K1[q], g.K2[q], g.kf[q], x, u, z);
       if (k == 0) u0 = u;
-      const double hi = in.hi[q], lo = in.lo[q];
-      const double r = (hi + lo) / 2;
-      g.w[q] = (in.f[q] == 0) ? z - r : u;
-      g.nf[q] = (z > hi + tol) ? 1 : ((z < lo - tol) ? 2 : 0);
+      const double d = z - in.r[q], ht = in.h[q] + tol;
+      g.w[q] = (in.f[q] == 0) ? d : u;
+      g.nf[q] = (d > ht) ? 1 : ((d < -ht) ? -1 : 0);
     }
   }
 }
@@ -387,7 +356,8 @@ __device__ __forceinline__ void seg_forward_tail(const LqArgs& a, const double* 
       double u, z;
       fwd_step(a, t[0], t[1], t[2], g.kf[q], x, u, z);
       if (k == 0) u0 = u;
-      const int nf = (z > in.hi[q] + tol) ? 1 : ((z < in.lo[q] - tol) ? 2 : 0);
+      const double d = z - in.r[q], ht = in.h[q] + tol;
+      const int nf = (d > ht) ? 1 : ((d < -ht) ? -1 : 0);
       fl.set(k, lane, nf);
       changed |= nf != 0;
       kl = nf ? k : kl;
@@ -407,14 +377,13 @@ __device__ __forceinline__ void seg_costate(const LqArgs& a, int j, const SegIn<
     const int k = j * S + q;
     if (FULL || k < a.N) {
       const int f = in.f[q];
-      const double hi = in.hi[q], lo = in.lo[q];
       // pinned: π e + ρ v + λ2_{k+1} = 0 (stationarity in v_k; B̄ᵀλ = λ2)
       const double e = (f == 0) ? g.w[q] : -fma(a.rho, g.w[q], lam[2]) * a.ipi;
       {
-        const double r = (hi + lo) / 2;
-        const double t = (f == 1) ? hi : lo;
-        const double nu = e - (t - r);  // ν / Q (meaningful at pinned slots only)
-        const bool rel = (f == 1 && nu < -a.tolnu) || (f == 2 && nu > a.tolnu);
+        const double sg = (double)f;
+        const double nu = fma(-sg, in.h[q], e);  // e − (t − r): ν / Q (pinned slots only)
+        // wrong-signed multiplier (ν < 0 at z_max, ν > 0 at z_min): σν < −tol; free: 0 < −tol
+        const bool rel = sg * nu < -a.tolnu;
         // the slot's new flag, written unconditionally (branch-free)
         const int nf = (f == 0) ? g.nf[q] : (rel ? 0 : f);
         fl.set(k, lane, nf);
@@ -530,7 +499,7 @@ __global__ void __launch_bounds__(64 * G, 2)
   const int N = a.N;
   // slot flags [NS·S][64] bytes (rows past N stay 0: the last segment's loads are unguarded)
   const int fbytes = a.NS * S;
-  const Flags fl{lq_smem + (size_t)wave * fbytes * 64};
+  const Flags fl{reinterpret_cast<signed char*>(lq_smem) + (size_t)wave * fbytes * 64};
   double* ck = a.ck + (size_t)gw * a.NS * kCkStride;
   const CkIO<NT> io{};
   int axis;
@@ -658,10 +627,12 @@ __global__ void __launch_bounds__(64 * G, 2)
         for (int j = 0; j < jt; ++j) {
           seg_load<S, true>(a, j, L, i, fl, cur);
           ck_load(io, ck, j, v, lane);
-          if (j < jfull)
+          // (a free-segment form here — free steps, no costate — spills at 256 VGPRs)
+          if (j < jfull) {
             seg_sweep_b<S, true>(a, j, v, cur, g, xs, u0, changed, kl, fl, lane);
-          else
+          } else {
             seg_sweep_b<S, false>(a, j, v, cur, g, xs, u0, changed, kl, fl, lane);
+          }
         }
 #pragma unroll 1
         for (int j = jt; j < a.NS; ++j) {
@@ -767,7 +738,9 @@ __global__ void zmpc_strict_lq_table_kernel(LqArgs a, double* tab) {
 
 // Stage bounds into the kernel's tiled layout: source elements (b, t, axis) at
 // b·sb + min(t, nsrc − 1)·st + axis·sa of z_max and z_min → dst[((axis·G + b/64)·rows + t)·64
-// + b%64] = (z_max, z_min) for t < rows.  64 walks × 16 rows per workgroup through LDS;
+// + b%64] = (r, h) for t < rows, r = (z_max + z_min)/2 the reference's z_ref
+// (zmp_controller.py:184) and h = (z_max − z_min)/2 (a pinned slot's target r ± h equals its
+// bound to an ulp; the primal check's tolerance is 1e-13).  64 walks × 16 rows per workgroup through LDS;
 // consecutive threads read consecutive source elements for the walk-contiguous [B, n, 2]
 // layout and write consecutive destination pairs.
 struct StageArgs {
@@ -795,7 +768,8 @@ __global__ void __launch_bounds__(256) zmpc_bounds_stage_kernel(StageArgs s) {
     if (b < s.B) {
       if (s.perm) b = s.perm[b];
       const int64_t e = b * s.sb + t * s.st + ax * s.sa;
-      v = make_double2(s.hi[e], s.lo[e]);
+      const double hi = s.hi[e], lo = s.lo[e];
+      v = make_double2((hi + lo) / 2, (hi - lo) / 2);
     }
     tile[ax][tt][w] = v;
   }
