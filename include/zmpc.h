@@ -134,8 +134,12 @@ int zmpc_plan_timings(const zmpc_plan* plan, float* dst_host, int32_t count);
  *                           one-wave-per-walk kernel (the cross-check of the split kernels)
  *   ZMPC_OPT_KICK_ORDER     strict rollouts: 1 = walks mapped to lanes in (kick step, kick)
  *                           order (default), 0 = input order
- *   ZMPC_OPT_STRICT_SOLVER  strict plans: 0 = the LQ active-set kernel, 1 = the reduced-
- *                           Cholesky z-space kernel (cross-check; horizons up to 512)
+ *   ZMPC_OPT_STRICT_SOLVER  strict plans: 0 = auto (small batches — up to 4096 (walk, axis)
+ *                           instances — the one-instance-per-wavefront reduced-Cholesky kernel,
+ *                           larger ones the LQ lane-per-instance kernel), 1 = the reduced-
+ *                           Cholesky tile kernel (16 instances per workgroup; cross-check),
+ *                           2 = the one-instance-per-wavefront kernel, 3 = the LQ kernel
+ *                           (1 and 2: horizons up to 512)
  * Returns ZMPC_EINVAL for an unknown option or value.
  */
 #define ZMPC_OPT_CORRELATION 0

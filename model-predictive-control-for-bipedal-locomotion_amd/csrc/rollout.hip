@@ -1677,10 +1677,12 @@ void launch_wide(hipStream_t s, RolloutArgs q, size_t lds, int64_t B, int cus) {
 // Walks of at most 64·8+1 samples (one correlation pass).  The split kernels (a 128-thread
 // workgroup per walk, one wave per axis) when their LDS fits the default 64 KiB ceiling:
 //   shared CoP (f precomputed): zmpc_rollout_unc_splitd_kernel<CW, true>;
-//   odd CW (fast-FIR dense form): one walk per workgroup, with the next-round prefetch when the
-//     batch takes at most two dispatch rounds (config 2: 29.6 → 26.9 µs, profiles/r3pf/; with
-//     more rounds the touched lines are evicted before use, B = 16384: 92 → 117 µs);
-//   even CW: the persistent kernel at 1–3 walks per resident slot, else one walk per workgroup.
+//   otherwise one walk per workgroup (odd CW: the fast-FIR dense form), with the next-round
+//     prefetch when the batch takes at most two dispatch rounds (config 2: 29.6 → 26.9 µs,
+//     profiles/r3pf/; with more rounds the touched lines are evicted before use, B = 16384:
+//     92 → 117 µs).  Round 4: even CW no longer take the persistent kernel (it has no prefetch;
+//     the horizon sweep's even-CW horizons were the slow ones, profiles/r4/); the diagnostics
+//     build keeps it behind ZMPC_PERSISTENT for A/B.
 // Otherwise (very long horizons) or with ZMPC_OPT_ROLLOUT_KERNEL = 1 (the cross-check):
 // zmpc_rollout_unc_kernel, one wave per walk.
 template <int CW>
@@ -1705,18 +1707,19 @@ void launch_unc(const RolloutGeom& g, size_t lds, hipStream_t s, RolloutArgs a, 
     hipLaunchKernelGGL(zmpc_rollout_unc_kernel<CW>, dim3((unsigned)a.B), dim3(64), lds, s, a);
     return;
   }
-  if ((CW & 1) == 0) {
+#ifdef ZMPC_DIAG
+  static const bool pers = getenv("ZMPC_PERSISTENT") != nullptr;  // A/B: round-3 even-CW rule
+  if ((CW & 1) == 0 && pers) {
     const int per_cu = occupancy(
         reinterpret_cast<const void*>(zmpc_rollout_unc_persd_kernel<CW>), 128, lds_split);
     const int64_t grid = (int64_t)std::max(cus, 1) * per_cu;
-    // persistent only for a few walks per workgroup: config 2 (2 per workgroup) 45 µs vs
-    // 49 µs; at 8 per workgroup (B = 16384) the one-walk grid is faster (156 vs 177 µs)
     if (per_cu > 0 && grid < a.B && a.B <= 3 * grid) {
       hipLaunchKernelGGL(zmpc_rollout_unc_persd_kernel<CW>, dim3((unsigned)grid), dim3(128),
                          lds_split, s, a);
       return;
     }
   }
+#endif
   const int occ = occupancy(
       reinterpret_cast<const void*>(zmpc_rollout_unc_splitd_kernel<CW, false>), 128, lds_split);
   const int64_t R = (int64_t)std::max(cus, 1) * occ;

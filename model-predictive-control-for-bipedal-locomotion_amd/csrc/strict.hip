@@ -797,6 +797,123 @@ __global__ void __launch_bounds__(256) zmpc_strict_kernel(StrictArgs a) {
   }
 }
 
+// ---- small batches: one instance per wavefront (north_star's mapping) -------------------------
+// The tile kernel above amortises the unconstrained solution over 16 instances with an MFMA GEMM;
+// with a handful of walks (the drop-in's single walk) most of those columns are empty and every
+// timestep pays the GEMM's and the gathers' L2 round trips.  Here a wave owns one instance
+// (walk, axis) for the whole rollout and a workgroup's waves share nothing but G, packed into LDS
+// once per workgroup (the lower triangle, N(N+1)/2 doubles: 90 KB at N = 150), so the
+// unconstrained solve D = G·W (each lane its horizon slots j = lane + 64c, G's row/column from
+// LDS), the reduced-matrix gathers and the row combinations of the active-set passes
+// (solve_instance, shared with the tile kernel) are LDS reads.  Same primal-dual active-set
+// iteration and warm start as the tile kernel and the LQ kernel: the same sets and solutions.
+constexpr int WWAVES = 4;  // instances (waves) per workgroup of the wave kernel
+
+template <int NJ>
+__global__ void __launch_bounds__(64 * WWAVES) zmpc_strict_wave_kernel(StrictArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int N = a.N, Np = a.Np;
+  // LDS carve: Gs [gsz] | per wave {W, zz, nuf, nuc, rj [Np], ia/iff [Np] ints, S [pcap],
+  //            x [4]} | st [WWAVES][Np] bytes
+  double* Gs = smem;
+  const int per_wave = 6 * Np + a.pcap + 4;
+  double* my = Gs + a.gsz + wave * per_wave;
+  double* W = my;
+  WaveWork w;
+  w.zz = my + Np;
+  w.nuf = my + 2 * Np;
+  w.nuc = my + 3 * Np;
+  w.rj = my + 4 * Np;
+  w.ia = reinterpret_cast<int*>(my + 5 * Np);
+  w.iff = w.ia + Np;
+  w.S = my + 6 * Np;
+  double* xs = w.S + a.pcap;
+  w.Sg = a.scratch + ((size_t)blockIdx.x * WWAVES + wave) * (size_t)a.sg_stride;
+  w.Gs = nullptr;
+  signed char* st = reinterpret_cast<signed char*>(Gs + a.gsz + WWAVES * per_wave) + wave * Np;
+  if (a.gsz > 0) {
+    for (int r = wave; r < N; r += WWAVES)
+      for (int c = lane; c <= r; c += 64) Gs[tri_at(r, c)] = a.G[(size_t)r * N + c];
+    w.Gs = Gs;
+  }
+  __syncthreads();  // (the last barrier: from here on every wave runs on its own)
+  const int64_t inst = (int64_t)blockIdx.x * WWAVES + wave;
+  if (inst >= a.ninst) return;
+  const int64_t nsteps = a.window_mode ? 1 : a.n - 1;
+  for (int j = lane; j < Np; j += 64) st[j] = 0;
+  if (lane < 3) xs[lane] = a.x0[inst * 3 + lane];
+  lds_sync();
+  if (!a.window_mode && lane < 3)  // hist[b, 0, axis, :] = x0
+    a.out[((inst >> 1) * a.n * 2 + (inst & 1)) * 3 + lane] = xs[lane];
+  const int64_t kstep = (!a.window_mode && (inst & 1) && a.kick != nullptr)
+                            ? (a.kick_steps ? a.kick_steps[inst >> 1] : a.kick_step)
+                            : -1;
+  const double kv = (kstep >= 0) ? a.kick[inst >> 1] : 0.0;
+  int fq = 0;
+  for (int64_t i = 0; i < nsteps; ++i) {
+    const double xv[3] = {xs[0], xs[1], xs[2]};
+    // W = Q (z_ref − c) of this window (zmp_controller.py:184, 197), then D = G W on the lane's
+    // horizon slots (G symmetric: G[j][k] from the packed lower triangle)
+    build_w<NJ>(a, inst, i, xv, W, lane);
+    lds_sync();
+    double d[NJ];
+#pragma unroll
+    for (int c = 0; c < NJ; ++c) d[c] = 0.0;
+    for (int j = 0; j < N; ++j) {
+      const double wj = W[j];
+#pragma unroll
+      for (int c = 0; c < NJ; ++c) {
+        const int k = lane + 64 * c;
+        if (k < N) d[c] = fma(g_at(a, w, k, j), wj, d[c]);
+      }
+    }
+    lds_sync();
+#pragma unroll
+    for (int c = 0; c < NJ; ++c)
+      if (lane + 64 * c < N) W[lane + 64 * c] = d[c];
+    // warm start: the previous set shifted one slot towards the present (slot N−1 kept)
+    if (i > 0) {
+      signed char v[NJ];
+#pragma unroll
+      for (int c = 0; c < NJ; ++c) {
+        const int j = lane + 64 * c;
+        v[c] = (j + 1 < N) ? st[j + 1] : ((j < N) ? st[j] : 0);
+      }
+      lds_sync();
+#pragma unroll
+      for (int c = 0; c < NJ; ++c)
+        if (lane + 64 * c < N) st[lane + 64 * c] = v[c];
+    }
+    lds_sync();
+    const double u0 = solve_instance<NJ>(a, inst, i, xv, W, st, w, lane, &fq);
+    double xn[3];
+    lipm_step(a.lc, xv, u0, xn);  // x⁺ = A x + B u0 (zmp_controller.py:199)
+    if (i == kstep) xn[1] -= kv;  // force kick (zmp_controller.py:90,105-106)
+    if (!(isfinite(xn[0]) && isfinite(xn[1]) && isfinite(xn[2]))) fq |= ZMPC_ST_NONFINITE;
+    lds_sync();
+    if (lane < 3) {
+      xs[lane] = xn[lane];
+      if (a.window_mode)
+        a.out[inst * 3 + lane] = xn[lane];
+      else
+        a.out[(((inst >> 1) * a.n + i + 1) * 2 + (inst & 1)) * 3 + lane] = xn[lane];
+    }
+    lds_sync();
+  }
+  if (a.status != nullptr && lane == 0) {
+    if (a.window_mode)
+      a.status[inst] = fq;
+    else if (fq != 0)
+      atomicOr(&a.status[inst >> 1], fq);
+  }
+}
+
+size_t wave_lds_bytes(int Np, int pcap, int gsz) {
+  return ((size_t)gsz + WWAVES * (6 * (size_t)Np + pcap + 4)) * sizeof(double) +
+         (size_t)WWAVES * Np;
+}
+
 size_t strict_lds_bytes(int Np, int ld, int pcap, int gsz) {
   const size_t per_wave = 5 * Np + (size_t)pcap;
   return ((size_t)gsz + SNB * ld + SNB * 4 + SNB + SWAVES * per_wave) * sizeof(double) +
@@ -814,6 +931,13 @@ hipError_t zmpc_strict_set_attrs() {
   ZMPC_SATTR(1) ZMPC_SATTR(2) ZMPC_SATTR(3) ZMPC_SATTR(4) ZMPC_SATTR(5) ZMPC_SATTR(6)
   ZMPC_SATTR(7) ZMPC_SATTR(8)
 #undef ZMPC_SATTR
+#define ZMPC_WATTR(J)                                                                   \
+  if (e == hipSuccess)                                                                  \
+    e = hipFuncSetAttribute((const void*)zmpc_strict_wave_kernel<J>,                   \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  ZMPC_WATTR(1) ZMPC_WATTR(2) ZMPC_WATTR(3) ZMPC_WATTR(4) ZMPC_WATTR(5) ZMPC_WATTR(6)
+  ZMPC_WATTR(7) ZMPC_WATTR(8)
+#undef ZMPC_WATTR
   return e;
 }
 
@@ -916,10 +1040,83 @@ static hipError_t launch_strict(const zmpc_plan* p, StrictArgs a, hipStream_t s,
   return e;
 }
 
-// ZMPC_OPT_STRICT_SOLVER = 1 (zmpc_plan_set_option) selects this file's reduced-Cholesky kernel
-// (cross-checks and A/B); the default is the LQ-form kernel of strict_lq.hip.
-static bool use_chol_variant(const zmpc_plan* p) {
-  return p->opt[ZMPC_OPT_STRICT_SOLVER] == 1 || !zmpc_strict_lq_supported(p);
+// The strict solver of a launch over `ninst` instances (ZMPC_OPT_STRICT_SOLVER: 1 the tile
+// kernel above, 2 the one-instance-per-wave kernel, 3 the LQ lane-per-instance kernel of
+// strict_lq.hip, 0 = auto): small batches take the wave kernel — each instance's active-set
+// passes spread over a wavefront, G in LDS — and large ones the LQ kernel, whose per-pass work is
+// O(N) per lane but serial within it.  Crossover (kWaveMaxInst) from the small-batch sweep,
+// scripts/strict_small_batch.py.
+constexpr int64_t kWaveMaxInst = 4096;
+enum { kTile = 1, kWave = 2, kLq = 3 };
+
+static int strict_mode(const zmpc_plan* p, int64_t ninst) {
+  const int opt = p->opt[ZMPC_OPT_STRICT_SOLVER];
+  const bool lq_ok = zmpc_strict_lq_supported(p);
+  if (opt == 1) return kTile;
+  if (opt == 2) return kWave;
+  if (opt == 3 && lq_ok) return kLq;
+  if (p->N <= 512 && (ninst <= kWaveMaxInst || !lq_ok)) return kWave;
+  return lq_ok ? kLq : kTile;
+}
+
+static hipError_t launch_strict_wave(const zmpc_plan* p, StrictArgs a, hipStream_t s,
+                                     std::string* why) {
+  if (p->N > 512) {
+    *why = "strict solver supports horizon N <= 512";
+    return hipErrorInvalidValue;
+  }
+  a.N = p->N;
+  a.Np = (p->N + 15) & ~15;
+  a.ld = a.Np;
+  a.Q = p->Q;
+  a.hg = p->hg;
+  a.lc = p->lc;
+  a.G = p->G;
+  a.Hz = p->Hz;
+  a.p0 = p->T3_6 - p->Thg;  // p(0) (zmp_controller.py:171, i = j)
+  a.lds_chol = 0;
+  a.dbg = nullptr;
+  const size_t budget = 160 * 1024 - 512;
+  // G packed in LDS when it fits beside a factor room for reduced systems of 32
+  const int gsz = ((p->N * (p->N + 1) / 2) + 1) & ~1;
+  a.gsz = wave_lds_bytes(a.Np, 32 * 33 / 2, gsz) <= budget ? gsz : 0;
+  if (wave_lds_bytes(a.Np, 0, a.gsz) > budget) {
+    *why = "horizon too long for the strict wave kernel's LDS (N=" + std::to_string(p->N) + ")";
+    return hipErrorInvalidValue;
+  }
+  // packed factor room for min(|A|, |F|) <= N/2 when it fits, else as much as fits (larger
+  // reduced systems factor in the wave's global scratch)
+  const int half = p->N / 2;
+  int pcap = half * (half + 1) / 2;
+  const int fit = (int)((budget - wave_lds_bytes(a.Np, 0, a.gsz)) / (WWAVES * sizeof(double)));
+  if (pcap > fit) pcap = fit;
+  a.pcap = pcap & ~1;
+  const int64_t grid = (a.ninst + WWAVES - 1) / WWAVES;
+  const int64_t half1 = p->N / 2 + 1;
+  a.sg_stride = half1 * half1;
+  const size_t sg_bytes = (size_t)grid * WWAVES * (size_t)a.sg_stride * sizeof(double);
+  if (hipMallocAsync((void**)&a.scratch, sg_bytes, s) != hipSuccess) {
+    (void)hipGetLastError();
+    return hipErrorOutOfMemory;
+  }
+  const size_t lds = wave_lds_bytes(a.Np, a.pcap, a.gsz);
+  switch ((a.N + 63) / 64) {
+#define ZMPC_WCASE(J)                                                                       \
+  case J:                                                                                   \
+    hipLaunchKernelGGL(zmpc_strict_wave_kernel<J>, dim3((unsigned)grid), dim3(64 * WWAVES), \
+                       lds, s, a);                                                          \
+    break;
+    ZMPC_WCASE(1) ZMPC_WCASE(2) ZMPC_WCASE(3) ZMPC_WCASE(4) ZMPC_WCASE(5) ZMPC_WCASE(6)
+    ZMPC_WCASE(7) ZMPC_WCASE(8)
+#undef ZMPC_WCASE
+    default:
+      (void)hipFreeAsync(a.scratch, s);
+      *why = "unsupported horizon";
+      return hipErrorInvalidValue;
+  }
+  hipError_t e = hipGetLastError();
+  const hipError_t ef = hipFreeAsync(a.scratch, s);
+  return e != hipSuccess ? e : ef;
 }
 
 hipError_t zmpc_launch_rollout_strict(const zmpc_plan* p, int64_t B, int64_t n,
@@ -927,7 +1124,8 @@ hipError_t zmpc_launch_rollout_strict(const zmpc_plan* p, int64_t B, int64_t n,
                                       const double* x0, const double* kick, int64_t kick_step,
                                       const int64_t* kick_steps, double* hist, int32_t* status,
                                       hipStream_t s, std::string* why) {
-  if (!use_chol_variant(p) && n > 1)
+  const int mode = strict_mode(p, 2 * B);
+  if (mode == kLq && n > 1)
     return zmpc_launch_rollout_strict_lq(p, B, n, zmax, zmin, bstride, x0, kick, kick_step,
                                          kick_steps, hist, status, s, why);
   if (!p->G) {
@@ -958,14 +1156,15 @@ hipError_t zmpc_launch_rollout_strict(const zmpc_plan* p, int64_t B, int64_t n,
   a.kick_steps = kick_steps;
   a.out = hist;
   a.status = status;
-  return launch_strict(p, a, s, why);
+  return mode == kWave ? launch_strict_wave(p, a, s, why) : launch_strict(p, a, s, why);
 }
 
 hipError_t zmpc_launch_step_strict(const zmpc_plan* p, int64_t B, const double* x,
                                    const double* zmax_win, const double* zmin_win,
                                    double* x_next, int32_t* status, hipStream_t s,
                                    std::string* why) {
-  if (!use_chol_variant(p))
+  const int mode = strict_mode(p, B);
+  if (mode == kLq)
     return zmpc_launch_step_strict_lq(p, B, x, zmax_win, zmin_win, x_next, status, s, why);
   if (!p->G) {
     *why = "plan was created without strict workspace";
@@ -982,5 +1181,5 @@ hipError_t zmpc_launch_step_strict(const zmpc_plan* p, int64_t B, const double* 
   a.kick_step = -1;
   a.out = x_next;
   a.status = status;
-  return launch_strict(p, a, s, why);
+  return mode == kWave ? launch_strict_wave(p, a, s, why) : launch_strict(p, a, s, why);
 }

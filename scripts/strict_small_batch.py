@@ -20,8 +20,8 @@ from mpc_bipedal.solver import Plan  # noqa: E402
 
 def main():
     N = int(os.environ.get("N", "150"))
-    sizes = [int(v) for v in os.environ.get("SIZES", "1,2,8,64,256,1024").split(",")]
-    solvers = [int(v) for v in os.environ.get("SOLVERS", "0,1").split(",")]
+    sizes = [int(v) for v in os.environ.get("SIZES", "1,2,8,64,256,1024,2048,4096").split(",")]
+    solvers = [int(v) for v in os.environ.get("SOLVERS", "2,3").split(",")]
     d = dict(bench.DEFAULT_JSON, horizon=N, strict=True)
     cfg = MPCConfig(**d)
     dev = torch.device("cuda", 0)

@@ -624,6 +624,7 @@ def test_strict_kick_order_same_results(shared):
     outs = []
     for mode in (1, 0):
         p = plan(150, strict=True, dt=dt).set_option("kick_order", mode)
+        p.set_option("strict_solver", 3)  # (the kick order is the LQ kernel's lane order)
         h, st = p.rollout(zmax, zmin, x0, kick=dt * F / M, kick_step=ks)
         c = p.counters()
         assert int(st.abs().max()) == 0
@@ -645,7 +646,7 @@ def test_strict_work_counters():
     B = 128
     zmax, zmin, x0, F, dt = synthetic_batch(B, 150, seed=11)
     n = zmax.shape[1]
-    p = plan(150, strict=True, dt=dt)
+    p = plan(150, strict=True, dt=dt).set_option("strict_solver", 3)  # the LQ kernel counts
     p.counters(reset=True)
     _, st = p.rollout(zmax, zmin, x0, kick=dt * F / M, kick_step=n // 2)
     c = p.counters(reset=True)
@@ -818,36 +819,59 @@ def test_strict_horizon_limit():
         plan(2561, strict=True)
 
 
-def test_strict_cholesky_variant_vs_oracle():
-    """The reduced-Cholesky strict kernel (strict.hip, ZMPC_OPT_STRICT_SOLVER = 1 — a cross-check
-    of the default LQ kernel) on the N = 64/150 walks and single solves of the reference-driven
-    fixtures and on the N = 400 long-horizon fixtures (its 320 < N <= 512 range)."""
+@pytest.mark.parametrize("solver", (1, 2, 3))
+def test_strict_solvers_vs_reference(solver):
+    """Every strict solver forced through ZMPC_OPT_STRICT_SOLVER — 1 the reduced-Cholesky tile
+    kernel (16 instances per workgroup, MFMA GEMM), 2 the one-instance-per-wavefront kernel
+    (the small-batch default), 3 the LQ lane-per-instance kernel (the large-batch default) — on
+    the reference-driven strict walks (N = 64/150, F = 0/400/800 N), the cold single solves,
+    and the N = 400 long-horizon fixtures: CoM RMSE ≤ 1e-9, single solves ≤ 1e-7 relative."""
     s = golden("strict_ref.npz")
     lg = golden("strict_long_ref.npz")
     for N in (64, 150):
         zx, zn = s[f"n{N}_zmax"], s[f"n{N}_zmin"]
         n, dt = len(zx), 1.5 / N
-        p = plan(N, strict=True).set_option("strict_solver", 1)
-        for F in (0, 400, 800):
-            h, st = p.rollout(zx, zn, np.zeros((1, 2, 3)), kick=np.array([dt * F / M]),
-                              kick_step=n // 2)
-            assert int(st.abs().max()) == 0
-            assert rmse(h.cpu().numpy()[0][:, :, 0], s[f"n{N}_F{F}_com"]) <= 1e-6, (N, F)
+        p = plan(N, strict=True).set_option("strict_solver", solver)
+        F = np.array([0.0, 400.0, 800.0])
+        h, st = p.rollout(zx, zn, np.zeros((3, 2, 3)), kick=dt * F / M, kick_step=n // 2)
+        assert int(st.abs().max()) == 0
+        for b, Fv in enumerate((0, 400, 800)):
+            assert rmse(h.cpu().numpy()[b][:, :, 0], s[f"n{N}_F{Fv}_com"]) <= 1e-9, (N, Fv)
         out, st = p.step(s[f"step{N}_x"], s[f"step{N}_zmax"], s[f"step{N}_zmin"])
         ref = s[f"step{N}_out"]
+        assert int(st.abs().max()) == 0
         assert np.abs(out.cpu().numpy() - ref).max() <= 1e-7 * max(1.0, np.abs(ref).max())
-    p = plan(400, strict=True).set_option("strict_solver", 1)
+    p = plan(400, strict=True).set_option("strict_solver", solver)
     zx, zn = lg["n400_zmax"], lg["n400_zmin"]
     n = len(zx)
     x0 = np.stack([lg["n400_x0"], lg["n400_y0"]])[None]
     h, st = p.rollout(zx, zn, x0, kick=np.array([float(lg["n400_kick"])]), kick_step=n // 2)
     assert int(st.abs().max()) == 0
-    assert rmse(h.cpu().numpy()[0][:, :, 0], lg["n400_com"]) <= 1e-6
+    assert rmse(h.cpu().numpy()[0][:, :, 0], lg["n400_com"]) <= 1e-9
     out, st = p.step(lg["step400_x"], lg["step400_zmax"], lg["step400_zmin"])
     ref = lg["step400_out"]
     assert np.abs(out.cpu().numpy() - ref).max() <= 1e-7 * max(1.0, np.abs(ref).max())
-    with pytest.raises(ValueError, match="reduced-Cholesky"):
-        plan(600, strict=True).set_option("strict_solver", 1)
+    if solver in (1, 2):
+        with pytest.raises(ValueError, match="reduced-Cholesky"):
+            plan(600, strict=True).set_option("strict_solver", solver)
+
+
+def test_strict_small_and_large_batch_paths_agree():
+    """The automatic choice (ZMPC_OPT_STRICT_SOLVER = 0) takes the wave kernel at small batches
+    and the LQ kernel at large ones; on one config-3 style batch of 300 walks both (forced) give
+    the same histories to rounding, and the automatic one equals the wave kernel's bitwise."""
+    zmax, zmin, x0, F, dt = synthetic_batch(300, 150, seed=41)
+    n = zmax.shape[1]
+    kick = dt * F / M
+    outs = {}
+    for solver in (0, 2, 3):
+        h, st = plan(150, strict=True, dt=dt).set_option("strict_solver", solver).rollout(
+            zmax, zmin, x0, kick=kick, kick_step=n // 2)
+        assert int(st.abs().max()) == 0
+        outs[solver] = h.cpu().numpy()
+    assert np.array_equal(outs[0], outs[2])
+    assert np.abs(outs[2] - outs[3]).max() <= 1e-9
+    assert rmse(outs[2][..., 0], outs[3][..., 0]) <= 1e-12
 
 
 @pytest.mark.parametrize("N,n", ((512, 1431), (150, 1100), (150, 2500), (256, 1000),
