@@ -759,6 +759,9 @@ def main():
                     help="also time batches pipelined two-deep on two streams (reported beside "
                          "value; off by default so a profile of the default command sees only "
                          "non-overlapped launches)")
+    ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
+                    help="plan option (mpc_bipedal/_native.py OPTIONS, include/zmpc.h "
+                         "ZMPC_OPT_*) for A/B timing of forms with the same results")
     args = ap.parse_args()
     if args.gpus < 1:
         raise SystemExit("--gpus must be >= 1")
@@ -824,6 +827,9 @@ def main():
     kick_h = cfg.dt * F_h / cfg.m
     plan = Plan(dev.index, cfg.horizon, cfg.dt, cfg.h, cfg.g, cfg.Q, cfg.R, cfg.strict)
     plan_rec = plan_record(plan)
+    for o in args.option:
+        name, _, val = o.partition("=")
+        plan.set_option(name, int(val))
     zmax = torch.as_tensor(zmax_h, device=dev)
     zmin = torch.as_tensor(zmin_h, device=dev)
     x0 = torch.as_tensor(x0_h, device=dev)
@@ -1017,6 +1023,7 @@ def main():
                 "samples_per_walk": n, "solves_per_step": solves_per_step,
                 "parallelism": f"dp{world}", "strict": bool(cfg.strict),
                 "shared_cop": bool(wl["shared"]),
+                **({"plan_options": args.option} if args.option else {}),
             },
             "roofline": roof,
             "cpu_baseline": cpu,

@@ -244,7 +244,7 @@ int zmpc_plan_timings(const zmpc_plan* P, float* dst, int32_t count) {
 int zmpc_plan_set_option(zmpc_plan* P, int32_t option, int64_t value) {
   g_err.clear();
   if (!P) return fail(ZMPC_EINVAL, "NULL plan");
-  static const int64_t hi[ZMPC_NOPTIONS] = {1, 3, 1, 1, 3};  // largest value of each option
+  static const int64_t hi[ZMPC_NOPTIONS] = {1, 3, 1, 1, 3, 2};  // largest value of each option
   if (option < 0 || option >= ZMPC_NOPTIONS) return fail(ZMPC_EINVAL, "unknown option");
   if (value < 0 || value > hi[option])
     return fail(ZMPC_EINVAL, "option value out of range (0.." + std::to_string(hi[option]) + ")");

@@ -41,7 +41,12 @@
 
 namespace {
 
-constexpr int HMAXIT = 64;  // default active-set pass cap (zmpc_herdt_params.max_passes)
+constexpr int HMAXIT = 64;
+#ifdef ZMPC_DIAG
+constexpr bool kProf = true;  // per-phase clocks (ZMPC_HERDT_PROF), diagnostics build only
+#else
+constexpr bool kProf = false;
+#endif  // default active-set pass cap (zmpc_herdt_params.max_passes)
 
 struct HerdtArgs {
   int N;
@@ -307,9 +312,12 @@ __device__ __forceinline__ void herdt_row(const RowC& c, double* P, double* s, d
     for (int q = 3; q < NA; ++q) Kh[q] = (foot && q - 3 == jf) ? -ip : 0.0;
     kff = -(t + cc0) * ip;
   }
-  double D[NA];
+  // D = Huu·K̂ − Hu (the pinned rows' correction; a free row's rounding residue), formed where
+  // it is used so that only Hu and K̂ stay live through the update
+#define HD(q) fma(Huu, Kh[q], -Hu[q])
+  // s first (hx dies before P's update)
 #pragma unroll
-  for (int q = 0; q < NA; ++q) D[q] = Huu * Kh[q] - Hu[q];
+  for (int q = 0; q < NA; ++q) s[q] = fma(-kff, HD(q), fma(-hu, Kh[q], hx[q]));
   // V_k: P = H − Hu K̂ᵀ + K̂ Dᵀ with H = ÂᵀPÂ + stage, updated in place block by block (each
   // block reads only its own old entries, so H is never held whole)
   {
@@ -318,7 +326,7 @@ __device__ __forceinline__ void herdt_row(const RowC& c, double* P, double* s, d
     const double q11 = P[sidx<NA>(1, 1)], q12 = P[sidx<NA>(1, 2)], q22 = P[sidx<NA>(2, 2)];
     const double a01 = T * q00 + q01, a02 = T2 * q00 + T * q01 + q02;  // (P A) row 0, cols 1, 2
     const double a11 = T * q01 + q11, a12 = T2 * q01 + T * q11 + q12;  // row 1
-    const double a21 = T * q02 + q12, a22 = T2 * q02 + T * q12 + q22;  // row 2
+    const double a22 = T2 * q02 + T * q12 + q22;                        // row 2
     double Hx[3][3];
     Hx[0][0] = q00;
     Hx[0][1] = a01;
@@ -326,13 +334,12 @@ __device__ __forceinline__ void herdt_row(const RowC& c, double* P, double* s, d
     Hx[1][1] = T * a01 + a11;
     Hx[1][2] = T * a02 + a12;
     Hx[2][2] = T2 * a02 + T * a12 + a22;
-    (void)a21;
 #pragma unroll
     for (int r = 0; r < 3; ++r)
 #pragma unroll
       for (int cc = r; cc < 3; ++cc) {
         const double v = Hx[r][cc] + be * ev[r] * ev[cc] + ga * c1[r] * c1[cc];
-        P[sidx<NA>(r, cc)] = v - Hu[r] * Kh[cc] + Kh[r] * D[cc];
+        P[sidx<NA>(r, cc)] = v - Hu[r] * Kh[cc] + Kh[r] * HD(cc);
       }
   }
 #pragma unroll
@@ -343,18 +350,18 @@ __device__ __forceinline__ void herdt_row(const RowC& c, double* P, double* s, d
     const double h0 = q0 + cf * c1[0];
     const double h1 = T * q0 + q1 + cf * c1[1];
     const double h2 = T2 * q0 + T * q1 + q2 + cf * c1[2];
-    P[sidx<NA>(0, cc)] = h0 - Hu[0] * Kh[cc] + Kh[0] * D[cc];
-    P[sidx<NA>(1, cc)] = h1 - Hu[1] * Kh[cc] + Kh[1] * D[cc];
-    P[sidx<NA>(2, cc)] = h2 - Hu[2] * Kh[cc] + Kh[2] * D[cc];
+    const double dc = HD(cc);
+    P[sidx<NA>(0, cc)] = h0 - Hu[0] * Kh[cc] + Kh[0] * dc;
+    P[sidx<NA>(1, cc)] = h1 - Hu[1] * Kh[cc] + Kh[1] * dc;
+    P[sidx<NA>(2, cc)] = h2 - Hu[2] * Kh[cc] + Kh[2] * dc;
     // f-f column cc (rows 3..cc)
 #pragma unroll
     for (int r = 3; r <= cc; ++r) {
       const double v = P[sidx<NA>(r, cc)] + ((r - 3 == jf && cc - 3 == jf) ? ga : 0.0);
-      P[sidx<NA>(r, cc)] = v - Hu[r] * Kh[cc] + Kh[r] * D[cc];
+      P[sidx<NA>(r, cc)] = v - Hu[r] * Kh[cc] + Kh[r] * dc;
     }
   }
-#pragma unroll
-  for (int q = 0; q < NA; ++q) s[q] = hx[q] - hu * Kh[q] - kff * D[q];
+#undef HD
   pbx[0] = pb[0];
   pbx[1] = pb[1];
   pbx[2] = pb[2];
@@ -476,7 +483,7 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
   int fq = 0;
   unsigned long long n_wave_pass = 0, n_pass = 0, n_m = 0, n_m2 = 0;
   unsigned itmax = 0;  // most passes of one solve (counter [9])
-  unsigned long long pr_b = 0, pr_f = 0, pr_w = 0, pr_t0 = a.prof ? clock64() : 0;
+  unsigned long long pr_b = 0, pr_f = 0, pr_w = 0, pr_t0 = (kProf && a.prof) ? clock64() : 0;
   unsigned long long pr_kw = 0, pr_ns = 0, pr_own = 0;
   const int64_t nsteps = a.window_mode ? 1 : a.n - 1;
   const int64_t kstep = (!a.window_mode && axis == 1 && a.kick) ? a.kick_step : -1;
@@ -550,7 +557,7 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
     bool pair_done = false;
     bool again = true;  // (itmax: the most passes of one solve, counter [9])
     while (again) {
-      const unsigned long long tp0 = a.prof ? clock64() : 0;
+      const unsigned long long tp0 = (kProf && a.prof) ? clock64() : 0;
       // ---- sweep 1: backward Riccati over ξ = [x; f] for V_0(x, f), then the footsteps -----
       // Run at the wave's footstep count (NW = 3 + mw columns, wave-uniform): lanes with fewer
       // footsteps carry zero columns, and no lane pays for the MM − mw columns nobody has.
@@ -585,7 +592,7 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
           herdt_row<NW>(rc, P, s, vr, (sg == 0) ? fc : 0.0, sg - 1, kd, wk, pbx, sb, Kx, kff);
           klane = (wk != 0 && klane < 0) ? k : klane;
         }
-        if (a.prof) tp1 = clock64();
+        if (kProf && a.prof) tp1 = clock64();
         // ---- footsteps: minimise V_0(x, f) over f, first footstep in the polytope (:771-783)
         double g[MW > 0 ? MW : 1];
 #pragma unroll
@@ -711,7 +718,7 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
       // Slab rows are loaded RB at a time: at one wave per SIMD nothing else hides the
       // latency of a row's loads.
       bool changed = false;
-      const unsigned long long tp2 = a.prof ? clock64() : 0;
+      const unsigned long long tp2 = (kProf && a.prof) ? clock64() : 0;
       {
         double xs[3] = {x[0], x[1], x[2]};
         // rows [kb, ke) in blocks of RB; TAIL: K from ktab (rows past the wave's last pinned
@@ -798,7 +805,7 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
         fwd(std::false_type{}, 0, kw + 1);
         fwd(std::true_type{}, kw + 1, N);
       }
-      if (a.prof) {
+      if (kProf && a.prof) {
         int kl = -1;
         for (int k = 0; k < N; ++k)
           if (wset[k * 64 + lane] != 0) kl = k;
@@ -814,7 +821,7 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
       }
       ++it;
       ++n_wave_pass;
-      if (a.prof) {
+      if (kProf && a.prof) {
         const bool pch = changed || (__shfl_xor(changed ? 1 : 0, 1, 64) != 0);
         if (!pair_done) {
           ++own;
@@ -894,7 +901,7 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
     const int other = __shfl(fq, lane ^ 1, 64);
     if (axis == 0) a.status[wc] = fq | other;
   }
-  if (a.prof) {
+  if (kProf && a.prof) {
     for (int o = 32; o > 0; o >>= 1) {
       pr_ns += __shfl_xor(pr_ns, o);
       pr_own += __shfl_xor(pr_own, o);

@@ -1045,8 +1045,10 @@ static hipError_t launch_strict(const zmpc_plan* p, StrictArgs a, hipStream_t s,
 // strict_lq.hip, 0 = auto): small batches take the wave kernel — each instance's active-set
 // passes spread over a wavefront, G in LDS — and large ones the LQ kernel, whose per-pass work is
 // O(N) per lane but serial within it.  Crossover (kWaveMaxInst) from the small-batch sweep,
-// scripts/strict_small_batch.py.
-constexpr int64_t kWaveMaxInst = 4096;
+// scripts/strict_small_batch.py (profiles/r4/r4e_strict_small_batch.jsonl, N = 150, n = 420:
+// 1 walk 27.6 vs 29.0 ms, 2 walks 28.2 vs 29.6, 8 walks 92.8 vs 46.4 — the wave kernel's passes
+// are long when a kicked walk pins many slots, and its workgroups then wait on the slowest).
+constexpr int64_t kWaveMaxInst = 4;
 enum { kTile = 1, kWave = 2, kLq = 3 };
 
 static int strict_mode(const zmpc_plan* p, int64_t ninst) {

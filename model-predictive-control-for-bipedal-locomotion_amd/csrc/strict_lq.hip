@@ -74,6 +74,12 @@ struct LqArgs {
   int64_t groups;        // groups per axis in the staging (1 for a shared CoP)
   int shared;            // 1: every walk reads group 0 (bounds_stride = 0)
   const double2* hl;
+  // run-length bounds (RUNS kernels): per (axis, group) [run][64] (z_ref, half-width) pairs and
+  // [run][64] start times (two INT_MAX sentinels after a lane's last run: the last run extends
+  // over the window padding of zmp_controller.py:81-88); rstride elements per (axis, group)
+  const double2* rs;
+  const int* rt;
+  int64_t rstride;
   const double* x0;      // rollout [B,2,3], step [B,3]
   const double* kick;    // [B] or null
   int64_t kick_step;
@@ -222,8 +228,89 @@ __device__ __forceinline__ void ric_tail(const LqArgs& a, Ric& v, double r, doub
 
 struct Lane {
   const double2* hl;  // wave's staged (z_ref, half-width) rows (uniform)
+  const double2* rs;  // RUNS: wave's run table (uniform)
+  const int* rt;
   int lane;
 };
+
+// RUNS: a lane's cursor on its walk's run list while a sweep moves through the window: the
+// current run's (z_ref, half-width), the neighbouring run the sweep reaches next and both
+// boundaries, so a crossing needs no load it must wait for (the refill of the neighbour lands
+// with the segment's checkpoint loads).  The CoP producer's bounds are one box per support
+// phase (cop_generator.py:34-115): ≈16 runs per 420-sample walk, so a sweep crosses a handful
+// of boundaries instead of loading one row per slot.
+struct RunCursor {
+  int ci;      // current run
+  int e1, e2;  // forward: starts of runs ci+1, ci+2; backward: starts of runs ci, ci−1
+  double r, h, nr, nh;
+};
+
+__device__ __forceinline__ RunCursor run_fwd(const Lane& L, int ci) {
+  RunCursor c;
+  c.ci = ci;
+  const double2 v = L.rs[ci * 64 + L.lane], w = L.rs[(ci + 1) * 64 + L.lane];
+  c.r = v.x;
+  c.h = v.y;
+  c.nr = w.x;
+  c.nh = w.y;
+  c.e1 = L.rt[(ci + 1) * 64 + L.lane];
+  c.e2 = L.rt[(ci + 2) * 64 + L.lane];
+  return c;
+}
+
+__device__ __forceinline__ RunCursor run_bwd(const Lane& L, int ci) {
+  RunCursor c;
+  c.ci = ci;
+  const int pi = max(ci - 1, 0);
+  const double2 v = L.rs[ci * 64 + L.lane], w = L.rs[pi * 64 + L.lane];
+  c.r = v.x;
+  c.h = v.y;
+  c.nr = w.x;
+  c.nh = w.y;
+  c.e1 = L.rt[ci * 64 + L.lane];
+  c.e2 = L.rt[pi * 64 + L.lane];
+  return c;
+}
+
+// Fill a segment's bounds from the runs (times t0 .. t0 + S − 1; backward sweeps descending).
+template <int S, bool FWD>
+__device__ __forceinline__ void seg_runs(const Lane& L, int t0, RunCursor& c, double* r,
+                                         double* h) {
+  if constexpr (FWD) {
+#pragma unroll
+    for (int q = 0; q < S; ++q) {
+      if (t0 + q >= c.e1) {  // into run ci+1 (runs are ≥ 1 slot: one crossing per slot)
+        ++c.ci;
+        c.r = c.nr;
+        c.h = c.nh;
+        c.e1 = c.e2;
+        const double2 w = L.rs[(c.ci + 1) * 64 + L.lane];
+        c.nr = w.x;
+        c.nh = w.y;
+        c.e2 = L.rt[(c.ci + 2) * 64 + L.lane];
+      }
+      r[q] = c.r;
+      h[q] = c.h;
+    }
+  } else {
+#pragma unroll
+    for (int q = S - 1; q >= 0; --q) {
+      if (t0 + q < c.e1) {  // into run ci−1
+        --c.ci;
+        c.r = c.nr;
+        c.h = c.nh;
+        c.e1 = c.e2;
+        const int pi = max(c.ci - 1, 0);
+        const double2 w = L.rs[pi * 64 + L.lane];
+        c.nr = w.x;
+        c.nh = w.y;
+        c.e2 = L.rt[pi * 64 + L.lane];
+      }
+      r[q] = c.r;
+      h[q] = c.h;
+    }
+  }
+}
 
 // Per-lane working-set flags of the wave's N slots in LDS (0 free, +1 at z_max, −1 at z_min):
 // one signed byte per slot, [slot][64].
@@ -250,6 +337,17 @@ __device__ __forceinline__ void seg_load(const LqArgs& a, int j, const Lane& L, 
     in.r[q] = v.x;
     in.h[q] = v.y;
     if (FLAGS) in.f[q] = fl.get(j * S + q, L.lane);
+  }
+}
+
+// The same from the run lists (RUNS): bounds from the lane's cursor, flags from LDS.
+template <int S, bool FLAGS, bool FWD>
+__device__ __forceinline__ void seg_load_runs(const LqArgs& a, int j, const Lane& L, int64_t i,
+                                              RunCursor& c, const Flags& fl, SegIn<S>& in) {
+  seg_runs<S, FWD>(L, (int)(i + a.toff) + j * S, c, in.r, in.h);
+  if (FLAGS) {
+#pragma unroll
+    for (int q = 0; q < S; ++q) in.f[q] = fl.get(j * S + q, L.lane);
   }
 }
 
@@ -490,7 +588,7 @@ __device__ __forceinline__ void ck_load_s(const CkIO<NT>& io, const double* ck, 
 // one wave of each axis — the y axis carries nearly all of the active-set work, and an
 // axis-pure SIMD would idle once its x waves are done (config 3: 117 → 98 ms, round 1).  Longer
 // horizons (slot flags of G waves beyond LDS) run G = 4 (x/y = wave parity), 2 or 1.
-template <int S, int G, bool NT>
+template <int S, int G, bool NT, bool RUNS>
 __global__ void __launch_bounds__(64 * G, 2)
     zmpc_strict_lq_kernel(LqArgs a, const double* __restrict__ tab) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lq_smem[];
@@ -522,8 +620,21 @@ __global__ void __launch_bounds__(64 * G, 2)
   L.lane = lane;
   {
     const int64_t g = a.shared ? 0 : (b0 >> 6);
-    const int64_t off = ((int64_t)axis * a.groups + g) * a.rows * 64;
-    L.hl = a.hl + off;
+    if constexpr (RUNS) {
+      const int64_t off = ((int64_t)axis * a.groups + g) * a.rstride;
+      L.rs = a.rs + off;
+      L.rt = a.rt + off;
+    } else {
+      L.hl = a.hl + ((int64_t)axis * a.groups + g) * a.rows * 64;
+    }
+  }
+  // RUNS: the run holding the window's last slot of the last segment (sweep A starts there)
+  // and the one holding its first slot (sweep B), advanced as the lane's timestep moves
+  int ra = 0, rb = 0;
+  if constexpr (RUNS) {
+    const int tA = (int)a.toff + a.NS * S - 1, tB = (int)a.toff;
+    while (L.rt[(ra + 1) * 64 + lane] <= tA) ++ra;
+    while (L.rt[(rb + 1) * 64 + lane] <= tB) ++rb;
   }
   const int jfull = N / S;  // segments [0, jfull) are full
   for (int k = 0; k < fbytes; ++k) fl.p[k * 64 + lane] = 0;
@@ -577,10 +688,15 @@ __global__ void __launch_bounds__(64 * G, 2)
         Ric v{0, 0, 0, 0, 0, 0, 0, 0, 0};
         SegIn<S> cur;
         SegOut<S> g;
+        RunCursor rc{};
+        if constexpr (RUNS) rc = run_bwd(L, ra);
         // sweep A, free tail: the s recursion, checkpoints of s
 #pragma unroll 1
         for (int j = a.NS - 1; j >= jt; --j) {
-          seg_load<S, false>(a, j, L, i, fl, cur);
+          if constexpr (RUNS)
+            seg_load_runs<S, false, false>(a, j, L, i, rc, fl, cur);
+          else
+            seg_load<S, false>(a, j, L, i, fl, cur);
           ck_store_s(io, ck, j, v, lane);
           if (j < jfull)
             seg_tail<S, true, false>(a, tab, j, v, cur, g);
@@ -599,7 +715,10 @@ __global__ void __launch_bounds__(64 * G, 2)
         // sweep A, working-set segments: full Riccati, checkpoints of (P, s)
 #pragma unroll 1
         for (int j = jt - 1; j >= 0; --j) {
-          seg_load<S, true>(a, j, L, i, fl, cur);
+          if constexpr (RUNS)
+            seg_load_runs<S, true, false>(a, j, L, i, rc, fl, cur);
+          else
+            seg_load<S, true>(a, j, L, i, fl, cur);
           ck_store(io, ck, j, v, lane);
           const bool fr = seg_free(cur);
           if (j < jfull) {
@@ -623,9 +742,13 @@ __global__ void __launch_bounds__(64 * G, 2)
           xs[1] = fma(-0.5, xi2, xi1);
           xs[2] = xi2;
         }
+        if constexpr (RUNS) rc = run_fwd(L, rb);
 #pragma unroll 1
         for (int j = 0; j < jt; ++j) {
-          seg_load<S, true>(a, j, L, i, fl, cur);
+          if constexpr (RUNS)
+            seg_load_runs<S, true, true>(a, j, L, i, rc, fl, cur);
+          else
+            seg_load<S, true>(a, j, L, i, fl, cur);
           ck_load(io, ck, j, v, lane);
           // (a free-segment form here — free steps, no costate — spills at 256 VGPRs)
           if (j < jfull) {
@@ -636,7 +759,10 @@ __global__ void __launch_bounds__(64 * G, 2)
         }
 #pragma unroll 1
         for (int j = jt; j < a.NS; ++j) {
-          seg_load<S, false>(a, j, L, i, fl, cur);
+          if constexpr (RUNS)
+            seg_load_runs<S, false, true>(a, j, L, i, rc, fl, cur);
+          else
+            seg_load<S, false>(a, j, L, i, fl, cur);
           ck_load_s(io, ck, j, v, lane);
           if (j < jfull) {
             seg_tail<S, true, true>(a, tab, j, v, cur, g);
@@ -671,6 +797,11 @@ __global__ void __launch_bounds__(64 * G, 2)
         h[2] = xn[2];
         ++i;
         it = 0;
+        if constexpr (RUNS) {
+          const int tA = (int)(i + a.toff) + a.NS * S - 1, tB = (int)(i + a.toff);
+          if (L.rt[(ra + 1) * 64 + lane] <= tA) ++ra;  // one slot per timestep: one run at most
+          if (L.rt[(rb + 1) * 64 + lane] <= tB) ++rb;
+        }
         if (i < a.nsteps) {
           // warm start: the converged set shifted one slot towards the present (slot N−1
           // kept), this lane's column only
@@ -783,6 +914,52 @@ __global__ void __launch_bounds__(256) zmpc_bounds_stage_kernel(StageArgs s) {
   }
 }
 
+// Run-length staging (RUNS kernels): one thread per (lane position, axis) walks its walk's n
+// samples once and writes the runs of equal (z_ref, half-width) — bitwise equality — into its
+// lane column of the (axis, group) table: rs[r][64], rt[r][64] = start time, then two INT_MAX
+// sentinels (the last run covers the window padding).  Positions past B get one dummy run.
+__global__ void __launch_bounds__(64) zmpc_runs_stage_kernel(StageArgs s, double2* rs, int* rt,
+                                                             int64_t rstride) {
+  const int lane = threadIdx.x;
+  const int64_t grp = blockIdx.x, ax = blockIdx.y;
+  const int64_t p = grp * 64 + lane;
+  double2* R = rs + (ax * s.G + grp) * rstride + lane;
+  int* Tt = rt + (ax * s.G + grp) * rstride + lane;
+  int count = 0;
+  if (p < s.B) {
+    const int64_t b = s.perm ? (int64_t)s.perm[p] : p;
+    double pr = 0.0, ph = 0.0;
+    for (int64_t t = 0; t < s.nsrc; ++t) {
+      const int64_t e = b * s.sb + t * s.st + ax * s.sa;
+      const double hi = s.hi[e], lo = s.lo[e];
+      const double r = (hi + lo) / 2, h = (hi - lo) / 2;  // z_ref (zmp_controller.py:184)
+      if (t == 0 || r != pr || h != ph) {
+        R[count * 64] = make_double2(r, h);
+        Tt[count * 64] = (int)t;
+        ++count;
+        pr = r;
+        ph = h;
+      }
+    }
+  } else {
+    R[0] = make_double2(0.0, 0.0);  // as the row staging's unused positions
+    Tt[0] = 0;
+    count = 1;
+  }
+  Tt[count * 64] = 0x7fffffff;
+  Tt[(count + 1) * 64] = 0x7fffffff;
+  R[count * 64] = make_double2(0.0, 0.0);  // (a forward cursor's neighbour, never used)
+}
+
+hipError_t stage_runs(const double* hi, const double* lo, int64_t sb, int64_t st, int64_t sa,
+                      int64_t nsrc, int64_t B, int naxes, double2* rs, int* rt, int64_t rstride,
+                      hipStream_t s, const int32_t* perm) {
+  StageArgs g{hi, lo, sb, st, sa, nsrc, B, (B + 63) / 64, 0, naxes, perm, nullptr};
+  hipLaunchKernelGGL(zmpc_runs_stage_kernel, dim3((unsigned)g.G, (unsigned)naxes), dim3(64), 0,
+                     s, g, rs, rt, rstride);
+  return hipGetLastError();
+}
+
 hipError_t stage(const double* hi, const double* lo, int64_t sb, int64_t st, int64_t sa,
                  int64_t nsrc, int64_t B, int64_t rows, int naxes, double2* dst, hipStream_t s,
                  const int32_t* perm = nullptr) {
@@ -798,10 +975,13 @@ struct LqVariant {
   int G;
   void (*kernel)(LqArgs, const double*);     // checkpoints cached (shared CoP, window mode)
   void (*kernel_nt)(LqArgs, const double*);  // checkpoints non-temporal (per-walk bounds)
+  void (*kernel_runs)(LqArgs, const double*);     // run-length bounds, cached checkpoints
+  void (*kernel_runs_nt)(LqArgs, const double*);  // run-length bounds, non-temporal
 };
 
-#define ZMPC_LQV(G) \
-  {G, zmpc_strict_lq_kernel<LQ_S, G, false>, zmpc_strict_lq_kernel<LQ_S, G, true>}
+#define ZMPC_LQV(G)                                                                        \
+  {G, zmpc_strict_lq_kernel<LQ_S, G, false, false>, zmpc_strict_lq_kernel<LQ_S, G, true, false>, \
+   zmpc_strict_lq_kernel<LQ_S, G, false, true>, zmpc_strict_lq_kernel<LQ_S, G, true, true>}
 const LqVariant kLqVariants[] = {
     ZMPC_LQV(8),  // default
     ZMPC_LQV(4),  // N up to 640
@@ -852,8 +1032,9 @@ hipError_t launch_lq(const zmpc_plan* p, LqArgs& a, int64_t waves, hipStream_t s
   const size_t lds = lq_lds_bytes(var->G, p->N);
   // rollouts over per-walk bounds: non-temporal checkpoints (see CkIO)
   const bool nt = !a.window_mode && !a.shared;
-  hipLaunchKernelGGL(nt ? var->kernel_nt : var->kernel, dim3((unsigned)blocks),
-                     dim3(64 * var->G), lds, s, a, (const double*)p->lqtab);
+  auto k = a.rs ? (nt ? var->kernel_runs_nt : var->kernel_runs) : (nt ? var->kernel_nt : var->kernel);
+  hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(64 * var->G), lds, s, a,
+                     (const double*)p->lqtab);
   return hipGetLastError();
 }
 
@@ -862,7 +1043,7 @@ hipError_t launch_lq(const zmpc_plan* p, LqArgs& a, int64_t waves, hipStream_t s
 hipError_t zmpc_strict_lq_set_attrs() {
   hipError_t e = hipSuccess;
   for (const LqVariant& c : kLqVariants)
-    for (auto k : {c.kernel, c.kernel_nt})
+    for (auto k : {c.kernel, c.kernel_nt, c.kernel_runs, c.kernel_runs_nt})
       if (e == hipSuccess)
         e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 160 * 1024);
@@ -914,7 +1095,15 @@ hipError_t zmpc_launch_rollout_strict_lq(const zmpc_plan* p, int64_t B, int64_t 
   if (!var) return hipErrorInvalidValue;
   const int64_t G = var->G;  // checkpoints for every wave of the launched blocks
   const size_t ck_doubles = (size_t)((waves + G - 1) / G * G) * a.NS * kCkStride;
-  const size_t st_doubles = (size_t)2 * a.groups * a.rows * 64 * 2;  // 2 axes, (hi, lo)
+  // bounds: rows (2 axes × rows × 64 (z_ref, half-width)) or runs (per (axis, group) up to
+  // n + 2 runs of a pair and a start time).  ZMPC_OPT_STRICT_BOUNDS 0 (auto): runs for per-walk
+  // bounds, rows for a shared CoP (profiles/r4/r4e_*: config 3 71.8 → 64.3 ms with runs, L2
+  // fetch 122 → 24 GB per launch; config 4's shared rows stay in L2: 80.5 ms rows, 87.1 runs)
+  const int bopt = p->opt[ZMPC_OPT_STRICT_BOUNDS];
+  const bool runs = bopt == 2 || (bopt == 0 && bstride != 0);
+  a.rstride = (n + 2) * 64;
+  const size_t st_doubles = runs ? (size_t)2 * a.groups * a.rstride * 3
+                                 : (size_t)2 * a.groups * a.rows * 64 * 2;
   // kick order (order.hip): walks with per-walk kicks sorted by (kick step, kick) onto lanes,
   // when there is more than one wave of them (ZMPC_OPT_KICK_ORDER = 0 keeps the input order)
   const bool ordered = p->opt[ZMPC_OPT_KICK_ORDER] != 0 && kick != nullptr && B > 64;
@@ -936,9 +1125,18 @@ hipError_t zmpc_launch_rollout_strict_lq(const zmpc_plan* p, int64_t B, int64_t 
                         ws + ck_doubles + st_doubles + perm_doubles, s);
     a.perm = perm;
   }
-  if (e == hipSuccess)
-    e = stage(zmax, zmin, bstride, 2, 1, n, Bst, a.rows, 2, hl, s, a.shared ? nullptr : a.perm);
-  a.hl = hl;
+  if (e == hipSuccess) {
+    const int32_t* perm = a.shared ? nullptr : a.perm;
+    if (runs) {
+      a.rs = hl;
+      a.rt = reinterpret_cast<int*>(hl + 2 * a.groups * a.rstride);
+      e = stage_runs(zmax, zmin, bstride, 2, 1, n, Bst, 2, hl, const_cast<int*>(a.rt), a.rstride,
+                     s, perm);
+    } else {
+      e = stage(zmax, zmin, bstride, 2, 1, n, Bst, a.rows, 2, hl, s, perm);
+      a.hl = hl;
+    }
+  }
   if (e == hipSuccess) e = launch_lq(p, a, waves, s);
   hipError_t ef = hipFreeAsync(ws, s);
   return e != hipSuccess ? e : ef;

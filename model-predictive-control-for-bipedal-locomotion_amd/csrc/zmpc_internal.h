@@ -72,7 +72,7 @@ struct zmpc_plan {
   // plan-build stage durations (zmpc_plan_timings), milliseconds
   float stage_ms[ZMPC_PLAN_STAGES] = {};
   // algorithm options (zmpc_plan_set_option), defaults as include/zmpc.h
-  int opt[ZMPC_NOPTIONS] = {0, 0, 0, 1, 0};
+  int opt[ZMPC_NOPTIONS] = {0, 0, 0, 1, 0, 0};
 };
 
 // rows of the fast-FIR tap table: m = 0..⌈(N+1)/2⌉−1, plus zero rows for an unrolled loop

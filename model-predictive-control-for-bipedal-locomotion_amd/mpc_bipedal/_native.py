@@ -35,7 +35,7 @@ EXPORT_P, EXPORT_PX, EXPORT_M, EXPORT_K, EXPORT_KX, EXPORT_G, EXPORT_L, EXPORT_H
 
 # zmpc_plan_set_option (include/zmpc.h ZMPC_OPT_*): algorithm selection, same solutions
 OPTIONS = {"correlation": 0, "long_walk": 1, "rollout_kernel": 2, "kick_order": 3,
-           "strict_solver": 4}
+           "strict_solver": 4, "strict_bounds": 5}
 
 # every symbol include/zmpc.h declares, with (restype, argtypes)
 _c_dbl_p = ctypes.c_void_p  # device pointers travel as integers

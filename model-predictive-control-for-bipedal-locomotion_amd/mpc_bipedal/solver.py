@@ -106,7 +106,7 @@ class Plan:
     def set_option(self, option, value: int) -> "Plan":
         """zmpc_plan_set_option: choose between forms that compute the same solution (cross-checks
         and A/B timing).  option: a name of _native.OPTIONS ("correlation", "long_walk",
-        "rollout_kernel", "kick_order", "strict_solver") or its ZMPC_OPT_* number."""
+        "rollout_kernel", "kick_order", "strict_solver", "strict_bounds") or its ZMPC_OPT_* number."""
         opt = _native.OPTIONS[option] if isinstance(option, str) else int(option)
         rc = _native.load().zmpc_plan_set_option(self._live(), opt, int(value))
         _native.check(rc, "zmpc_plan_set_option")

@@ -1,5 +1,5 @@
 """Diagnostic driver for profilers: a config-3-shaped strict rollout (B walks from argv,
-default 2048), two launches, whatever ZMPC_* env vars the caller set."""
+default 2048), two launches; further arguments NAME=VALUE are plan options (_native.OPTIONS)."""
 import os
 import sys
 
@@ -19,6 +19,9 @@ cfg = MPCConfig(**d)
 _, _, zmax, zmin, x0, F = make_batch(B, 0, cfg, False)
 n = zmax.shape[1]
 p = Plan(0, cfg.horizon, cfg.dt, cfg.h, cfg.g, cfg.Q, cfg.R, True)
+for o in sys.argv[2:]:
+    name, _, val = o.partition("=")
+    p.set_option(name, int(val))
 L = p.rollout_launcher(torch.as_tensor(zmax, device="cuda"), torch.as_tensor(zmin, device="cuda"),
                        torch.as_tensor(x0, device="cuda"),
                        kick=torch.as_tensor(cfg.dt * F / cfg.m, device="cuda"), kick_step=n // 2)

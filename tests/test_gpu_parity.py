@@ -640,6 +640,35 @@ def test_strict_kick_order_same_results(shared):
     assert rmse(hs[b, :, :, 0], ref[:, :, 0]) <= 1e-9
 
 
+@pytest.mark.parametrize("shared,N", ((False, 150), (True, 150), (False, 10)))
+def test_strict_run_length_bounds_same_results(shared, N):
+    """ZMPC_OPT_STRICT_BOUNDS: the LQ kernel reading the bounds as runs of equal values (2)
+    and as one staged row per sample (1) give bitwise the same histories and work — per-walk
+    bounds (kick-ordered lanes, a batch that is not a multiple of 64, walks whose bounds
+    change every sample in part) and the shared CoP, a horizon that is not a multiple of the
+    segment."""
+    B = 333
+    zmax, zmin, x0, F, dt = synthetic_batch(B, N, seed=31)
+    n = zmax.shape[1]
+    rng = np.random.default_rng(32)
+    F = rng.uniform(-800.0, 800.0, B)
+    ks = rng.integers(n // 4, 3 * n // 4, B).astype(np.int64)
+    if shared:
+        zmax, zmin, x0 = zmax[0], zmin[0], np.zeros_like(x0)
+    else:  # a few walks with a ramp in their bounds: one run per sample
+        ramp = 0.01 * np.sin(np.arange(n) * 0.3)
+        zmax[5:9, :, 0] += ramp
+        zmin[5:9, :, 0] += ramp
+    outs = []
+    for mode in (1, 2):
+        p = plan(N, strict=True, dt=dt).set_option("strict_solver", 3)
+        p.set_option("strict_bounds", mode)
+        h, st = p.rollout(zmax, zmin, x0, kick=dt * F / M, kick_step=ks)
+        outs.append((h.cpu().numpy(), st.cpu().numpy(), p.counters()["instance_passes"]))
+    (h1, s1, c1), (h2, s2, c2) = outs
+    assert np.array_equal(h1, h2) and np.array_equal(s1, s2) and c1 == c2
+
+
 def test_strict_work_counters():
     """zmpc_plan_counters: every solve takes at least one active-set pass; the working-set
     slots are a part of all pass-slots; reset zeroes them."""
@@ -856,11 +885,12 @@ def test_strict_solvers_vs_reference(solver):
             plan(600, strict=True).set_option("strict_solver", solver)
 
 
-def test_strict_small_and_large_batch_paths_agree():
-    """The automatic choice (ZMPC_OPT_STRICT_SOLVER = 0) takes the wave kernel at small batches
-    and the LQ kernel at large ones; on one config-3 style batch of 300 walks both (forced) give
-    the same histories to rounding, and the automatic one equals the wave kernel's bitwise."""
-    zmax, zmin, x0, F, dt = synthetic_batch(300, 150, seed=41)
+@pytest.mark.parametrize("B,auto", ((2, 2), (300, 3)))
+def test_strict_small_and_large_batch_paths_agree(B, auto):
+    """The automatic choice (ZMPC_OPT_STRICT_SOLVER = 0) takes the small-batch kernel at a few
+    instances and the LQ kernel beyond; on config-3 style batches both (forced) give the same
+    histories to rounding, and the automatic one equals the chosen kernel's bitwise."""
+    zmax, zmin, x0, F, dt = synthetic_batch(B, 150, seed=41)
     n = zmax.shape[1]
     kick = dt * F / M
     outs = {}
@@ -869,7 +899,7 @@ def test_strict_small_and_large_batch_paths_agree():
             zmax, zmin, x0, kick=kick, kick_step=n // 2)
         assert int(st.abs().max()) == 0
         outs[solver] = h.cpu().numpy()
-    assert np.array_equal(outs[0], outs[2])
+    assert np.array_equal(outs[0], outs[auto])
     assert np.abs(outs[2] - outs[3]).max() <= 1e-9
     assert rmse(outs[2][..., 0], outs[3][..., 0]) <= 1e-12
 
