@@ -134,12 +134,13 @@ int zmpc_plan_timings(const zmpc_plan* plan, float* dst_host, int32_t count);
  *                           one-wave-per-walk kernel (the cross-check of the split kernels)
  *   ZMPC_OPT_KICK_ORDER     strict rollouts: 1 = walks mapped to lanes in (kick step, kick)
  *                           order (default), 0 = input order
- *   ZMPC_OPT_STRICT_SOLVER  strict plans: 0 = auto (small batches — up to 4 (walk, axis)
- *                           instances — the one-instance-per-wavefront reduced-Cholesky kernel,
+ *   ZMPC_OPT_STRICT_SOLVER  strict plans: 0 = auto (small batches — up to 4096 (walk, axis)
+ *                           instances — the parallel-in-time one-instance-per-wavefront kernel,
  *                           larger ones the LQ lane-per-instance kernel), 1 = the reduced-
  *                           Cholesky tile kernel (16 instances per workgroup; cross-check),
- *                           2 = the one-instance-per-wavefront kernel, 3 = the LQ kernel
- *                           (1 and 2: horizons up to 512)
+ *                           2 = the reduced-Cholesky one-instance-per-wavefront kernel
+ *                           (cross-check), 3 = the LQ kernel, 4 = the parallel-in-time kernel
+ *                           (1, 2 and 4: horizons up to 512)
  *   ZMPC_OPT_STRICT_BOUNDS  strict rollouts on the LQ kernel: 0 = auto (run-length for per-walk
  *                           bounds, rows for a shared CoP), 1 = the bounds staged one row per
  *                           sample, 2 = run-length bounds (one entry per run of equal bounds);

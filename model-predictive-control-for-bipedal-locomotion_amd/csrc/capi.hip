@@ -244,13 +244,14 @@ int zmpc_plan_timings(const zmpc_plan* P, float* dst, int32_t count) {
 int zmpc_plan_set_option(zmpc_plan* P, int32_t option, int64_t value) {
   g_err.clear();
   if (!P) return fail(ZMPC_EINVAL, "NULL plan");
-  static const int64_t hi[ZMPC_NOPTIONS] = {1, 3, 1, 1, 3, 2};  // largest value of each option
+  static const int64_t hi[ZMPC_NOPTIONS] = {1, 3, 1, 1, 4, 2};  // largest value of each option
   if (option < 0 || option >= ZMPC_NOPTIONS) return fail(ZMPC_EINVAL, "unknown option");
   if (value < 0 || value > hi[option])
     return fail(ZMPC_EINVAL, "option value out of range (0.." + std::to_string(hi[option]) + ")");
-  if (option == ZMPC_OPT_STRICT_SOLVER && (value == 1 || value == 2) &&
+  if (option == ZMPC_OPT_STRICT_SOLVER && (value == 1 || value == 2 || value == 4) &&
       (!P->strict || P->N > 512))
-    return fail(ZMPC_EINVAL, "the reduced-Cholesky strict kernels need a strict plan, N <= 512");
+    return fail(ZMPC_EINVAL, "the small-batch and reduced-Cholesky strict kernels need a strict "
+                             "plan, N <= 512");
   P->opt[option] = (int)value;
   return ZMPC_OK;
 }

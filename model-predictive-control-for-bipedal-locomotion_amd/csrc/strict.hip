@@ -1041,23 +1041,27 @@ static hipError_t launch_strict(const zmpc_plan* p, StrictArgs a, hipStream_t s,
 }
 
 // The strict solver of a launch over `ninst` instances (ZMPC_OPT_STRICT_SOLVER: 1 the tile
-// kernel above, 2 the one-instance-per-wave kernel, 3 the LQ lane-per-instance kernel of
-// strict_lq.hip, 0 = auto): small batches take the wave kernel — each instance's active-set
-// passes spread over a wavefront, G in LDS — and large ones the LQ kernel, whose per-pass work is
-// O(N) per lane but serial within it.  Crossover (kWaveMaxInst) from the small-batch sweep,
-// scripts/strict_small_batch.py (profiles/r4/r4e_strict_small_batch.jsonl, N = 150, n = 420:
-// 1 walk 27.6 vs 29.0 ms, 2 walks 28.2 vs 29.6, 8 walks 92.8 vs 46.4 — the wave kernel's passes
-// are long when a kicked walk pins many slots, and its workgroups then wait on the slowest).
-constexpr int64_t kWaveMaxInst = 4;
-enum { kTile = 1, kWave = 2, kLq = 3 };
+// kernel above, 2 the reduced-Cholesky one-instance-per-wave kernel, 3 the LQ lane-per-instance
+// kernel of strict_lq.hip, 4 the parallel-in-time one-instance-per-wave kernel of
+// strict_scan.hip, 0 = auto): small batches take the parallel-in-time kernel and large ones the
+// LQ kernel, whose per-pass work is O(N) per lane but serial within it.  The reduced-Cholesky
+// wave kernel is a cross-check (profiles/r4/r4e_strict_small_batch.jsonl, N = 150, n = 420: 1
+// walk 27.6 ms vs the LQ kernel's 29.0, 8 walks 92.8 vs 46.4 — its passes are long when a
+// kicked walk pins many slots).
+// Option 4 / auto at up to kScanMaxInst instances: the parallel-in-time kernel of
+// strict_scan.hip (one instance per wave, the horizon over the lanes).
+constexpr int64_t kScanMaxInst = 0;  // (pending measurement)
+enum { kTile = 1, kWave = 2, kLq = 3, kScan = 4 };
 
 static int strict_mode(const zmpc_plan* p, int64_t ninst) {
   const int opt = p->opt[ZMPC_OPT_STRICT_SOLVER];
   const bool lq_ok = zmpc_strict_lq_supported(p);
+  const bool scan_ok = zmpc_strict_scan_supported(p);
   if (opt == 1) return kTile;
   if (opt == 2) return kWave;
   if (opt == 3 && lq_ok) return kLq;
-  if (p->N <= 512 && (ninst <= kWaveMaxInst || !lq_ok)) return kWave;
+  if (opt == 4 && scan_ok) return kScan;
+  if (scan_ok && (ninst <= kScanMaxInst || !lq_ok)) return kScan;
   return lq_ok ? kLq : kTile;
 }
 
@@ -1127,6 +1131,9 @@ hipError_t zmpc_launch_rollout_strict(const zmpc_plan* p, int64_t B, int64_t n,
                                       const int64_t* kick_steps, double* hist, int32_t* status,
                                       hipStream_t s, std::string* why) {
   const int mode = strict_mode(p, 2 * B);
+  if (mode == kScan && n > 1)
+    return zmpc_launch_rollout_strict_scan(p, B, n, zmax, zmin, bstride, x0, kick, kick_step,
+                                           kick_steps, hist, status, s, why);
   if (mode == kLq && n > 1)
     return zmpc_launch_rollout_strict_lq(p, B, n, zmax, zmin, bstride, x0, kick, kick_step,
                                          kick_steps, hist, status, s, why);
@@ -1166,6 +1173,8 @@ hipError_t zmpc_launch_step_strict(const zmpc_plan* p, int64_t B, const double* 
                                    double* x_next, int32_t* status, hipStream_t s,
                                    std::string* why) {
   const int mode = strict_mode(p, B);
+  if (mode == kScan)
+    return zmpc_launch_step_strict_scan(p, B, x, zmax_win, zmin_win, x_next, status, s, why);
   if (mode == kLq)
     return zmpc_launch_step_strict_lq(p, B, x, zmax_win, zmin_win, x_next, status, s, why);
   if (!p->G) {

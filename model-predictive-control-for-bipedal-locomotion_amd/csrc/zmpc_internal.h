@@ -137,6 +137,19 @@ hipError_t zmpc_strict_lq_set_attrs();
 size_t zmpc_strict_lq_table_doubles(int N);
 hipError_t zmpc_strict_lq_build_table(zmpc_plan* p, hipStream_t s);
 
+// strict box-QP for small batches, one instance per wave, parallel in time (strict_scan.hip)
+hipError_t zmpc_launch_rollout_strict_scan(const zmpc_plan* p, int64_t B, int64_t n,
+                                           const double* zmax, const double* zmin,
+                                           int64_t bstride, const double* x0, const double* kick,
+                                           int64_t kick_step, const int64_t* kick_steps,
+                                           double* hist, int32_t* status, hipStream_t s,
+                                           std::string* why);
+hipError_t zmpc_launch_step_strict_scan(const zmpc_plan* p, int64_t B, const double* x,
+                                        const double* zmax_win, const double* zmin_win,
+                                        double* x_next, int32_t* status, hipStream_t s,
+                                        std::string* why);
+bool zmpc_strict_scan_supported(const zmpc_plan* p);
+
 // walk order for the lane-per-instance kernels (order.hip): perm[B] = the walks sorted by
 // (kick step, kick), so that a wave's lanes take similar disturbances; ws of
 // zmpc_kick_order_bytes(B) bytes (device, stream-ordered)

@@ -1,8 +1,9 @@
 """Strict rollouts at small batches (the drop-in's single walk up to ~1024 walks): kernel time of
 each strict solver per batch size, one JSON line per (solver, B).  Default.json CoP at N = 150
 with config-3 style offsets, x0 and F_ext (bench.py make_batch).  Solvers: the plan option
-ZMPC_OPT_STRICT_SOLVER (0 = LQ lane-per-instance kernel, 1 = reduced-Cholesky z-space kernel)
-and, when present, the small-batch path chosen automatically (option absent → default)."""
+ZMPC_OPT_STRICT_SOLVER (4 = the parallel-in-time one-instance-per-wave kernel, 3 = the LQ
+lane-per-instance kernel, 2 = the reduced-Cholesky one-instance-per-wave kernel), then the
+drop-in single walk (automatic choice)."""
 import json
 import os
 import sys
@@ -21,7 +22,7 @@ from mpc_bipedal.solver import Plan  # noqa: E402
 def main():
     N = int(os.environ.get("N", "150"))
     sizes = [int(v) for v in os.environ.get("SIZES", "1,2,8,64,256,1024,2048,4096").split(",")]
-    solvers = [int(v) for v in os.environ.get("SOLVERS", "2,3").split(",")]
+    solvers = [int(v) for v in os.environ.get("SOLVERS", "4,3,2").split(",")]
     d = dict(bench.DEFAULT_JSON, horizon=N, strict=True)
     cfg = MPCConfig(**d)
     dev = torch.device("cuda", 0)

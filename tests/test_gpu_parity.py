@@ -848,11 +848,12 @@ def test_strict_horizon_limit():
         plan(2561, strict=True)
 
 
-@pytest.mark.parametrize("solver", (1, 2, 3))
+@pytest.mark.parametrize("solver", (1, 2, 3, 4))
 def test_strict_solvers_vs_reference(solver):
     """Every strict solver forced through ZMPC_OPT_STRICT_SOLVER — 1 the reduced-Cholesky tile
-    kernel (16 instances per workgroup, MFMA GEMM), 2 the one-instance-per-wavefront kernel
-    (the small-batch default), 3 the LQ lane-per-instance kernel (the large-batch default) — on
+    kernel (16 instances per workgroup, MFMA GEMM), 2 the reduced-Cholesky one-instance-per-
+    wavefront kernel, 3 the LQ lane-per-instance kernel (the large-batch default), 4 the
+    parallel-in-time one-instance-per-wavefront kernel (the small-batch default) — on
     the reference-driven strict walks (N = 64/150, F = 0/400/800 N), the cold single solves,
     and the N = 400 long-horizon fixtures: CoM RMSE ≤ 1e-9, single solves ≤ 1e-7 relative."""
     s = golden("strict_ref.npz")
@@ -880,28 +881,30 @@ def test_strict_solvers_vs_reference(solver):
     out, st = p.step(lg["step400_x"], lg["step400_zmax"], lg["step400_zmin"])
     ref = lg["step400_out"]
     assert np.abs(out.cpu().numpy() - ref).max() <= 1e-7 * max(1.0, np.abs(ref).max())
-    if solver in (1, 2):
+    if solver in (1, 2, 4):
         with pytest.raises(ValueError, match="reduced-Cholesky"):
             plan(600, strict=True).set_option("strict_solver", solver)
 
 
-@pytest.mark.parametrize("B,auto", ((2, 2), (300, 3)))
+@pytest.mark.parametrize("B,auto", ((2, 4), (300, 4), (2100, 3)))
 def test_strict_small_and_large_batch_paths_agree(B, auto):
-    """The automatic choice (ZMPC_OPT_STRICT_SOLVER = 0) takes the small-batch kernel at a few
-    instances and the LQ kernel beyond; on config-3 style batches both (forced) give the same
-    histories to rounding, and the automatic one equals the chosen kernel's bitwise."""
+    """The automatic choice (ZMPC_OPT_STRICT_SOLVER = 0) takes the parallel-in-time kernel up to
+    4096 instances and the LQ kernel beyond; on config-3 style batches the small-batch kernels
+    (forced) and the LQ kernel give the same histories to rounding, and the automatic one equals
+    the chosen kernel's bitwise."""
     zmax, zmin, x0, F, dt = synthetic_batch(B, 150, seed=41)
     n = zmax.shape[1]
     kick = dt * F / M
     outs = {}
-    for solver in (0, 2, 3):
+    for solver in ((0, 2, 3, 4) if B <= 300 else (0, 3, 4)):
         h, st = plan(150, strict=True, dt=dt).set_option("strict_solver", solver).rollout(
             zmax, zmin, x0, kick=kick, kick_step=n // 2)
         assert int(st.abs().max()) == 0
         outs[solver] = h.cpu().numpy()
     assert np.array_equal(outs[0], outs[auto])
-    assert np.abs(outs[2] - outs[3]).max() <= 1e-9
-    assert rmse(outs[2][..., 0], outs[3][..., 0]) <= 1e-12
+    for sv in outs:
+        assert np.abs(outs[sv] - outs[3]).max() <= 1e-9, sv
+        assert rmse(outs[sv][..., 0], outs[3][..., 0]) <= 1e-12, sv
 
 
 @pytest.mark.parametrize("N,n", ((512, 1431), (150, 1100), (150, 2500), (256, 1000),
