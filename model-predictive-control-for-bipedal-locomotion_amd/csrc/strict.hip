@@ -1050,7 +1050,7 @@ static hipError_t launch_strict(const zmpc_plan* p, StrictArgs a, hipStream_t s,
 // kicked walk pins many slots).
 // Option 4 / auto at up to kScanMaxInst instances: the parallel-in-time kernel of
 // strict_scan.hip (one instance per wave, the horizon over the lanes).
-constexpr int64_t kScanMaxInst = 0;  // (pending measurement)
+constexpr int64_t kScanMaxInst = 4096;
 enum { kTile = 1, kWave = 2, kLq = 3, kScan = 4 };
 
 static int strict_mode(const zmpc_plan* p, int64_t ninst) {

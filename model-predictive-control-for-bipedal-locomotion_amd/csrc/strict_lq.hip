@@ -55,8 +55,14 @@ namespace {
 using namespace zmpc_eta;
 
 constexpr int LQ_MAXIT = 64;  // active-set pass cap (as strict.hip)
-constexpr int LQ_S = 8;       // Riccati steps per checkpoint segment
-constexpr int LQ_DRIFT = 4;   // timesteps a lane may run ahead of its wave's slowest lane
+#ifndef ZMPC_LQ_S  // (A/B builds only: make ab)
+#define ZMPC_LQ_S 8
+#endif
+#ifndef ZMPC_LQ_DRIFT
+#define ZMPC_LQ_DRIFT 4
+#endif
+constexpr int LQ_S = ZMPC_LQ_S;  // Riccati steps per checkpoint segment
+constexpr int LQ_DRIFT = ZMPC_LQ_DRIFT;  // timesteps a lane may run ahead of its wave's slowest lane
                               // (round 3, profiles/r3u/, r3drift/: 0/1/2/4/8 → 104.5/94.8/92.5/
                               // 90.9/92.7 ms at config 3 — the bound rows stay a few rows apart)
 constexpr int TAB = 16;       // doubles per slot of the free-tail table: [0..2] K, [3] 1/Quu,

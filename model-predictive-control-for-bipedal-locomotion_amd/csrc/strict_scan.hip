@@ -367,17 +367,26 @@ __global__ void __launch_bounds__(64) zmpc_strict_scan_kernel(ScanArgs a) {
           shfl_down_elem(E, P, d);
           if (lane + d < 64) combine(E, P);
         }
-        // V at the chunk's end = the right neighbour's suffix (0 past the horizon)
-        const bool last = lane == 63;
-        v.p00 = last ? 0.0 : __shfl_down(E.J[0], 1, 64);
-        v.p01 = last ? 0.0 : __shfl_down(E.J[1], 1, 64);
-        v.p02 = last ? 0.0 : __shfl_down(E.J[2], 1, 64);
-        v.p11 = last ? 0.0 : __shfl_down(E.J[3], 1, 64);
-        v.p12 = last ? 0.0 : __shfl_down(E.J[4], 1, 64);
-        v.p22 = last ? 0.0 : __shfl_down(E.J[5], 1, 64);
-        v.s0 = last ? 0.0 : __shfl_down(E.g[0], 1, 64);
-        v.s1 = last ? 0.0 : __shfl_down(E.g[1], 1, 64);
-        v.s2 = last ? 0.0 : __shfl_down(E.g[2], 1, 64);
+        // V at the chunk's end = the right neighbour's suffix (0 past the horizon).  Every lane
+        // takes part in the shuffles (a source lane outside the exec mask reads as 0); the last
+        // lane's result is replaced afterwards.
+        {
+          double vv[9];
+#pragma unroll
+          for (int q = 0; q < 6; ++q) vv[q] = __shfl_down(E.J[q], 1, 64);
+#pragma unroll
+          for (int q = 0; q < 3; ++q) vv[6 + q] = __shfl_down(E.g[q], 1, 64);
+          const bool last = lane == 63;
+          v.p00 = last ? 0.0 : vv[0];
+          v.p01 = last ? 0.0 : vv[1];
+          v.p02 = last ? 0.0 : vv[2];
+          v.p11 = last ? 0.0 : vv[3];
+          v.p12 = last ? 0.0 : vv[4];
+          v.p22 = last ? 0.0 : vv[5];
+          v.s0 = last ? 0.0 : vv[6];
+          v.s1 = last ? 0.0 : vv[7];
+          v.s2 = last ? 0.0 : vv[8];
+        }
       }
       // ---- the lane's slots: Riccati back from V_end; keep the laws and V_{k+1}'s last column
       double K0[C], K1[C], K2[C], kf[C], vp02[C], vp12[C], vp22[C], vs2[C];

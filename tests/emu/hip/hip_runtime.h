@@ -1,0 +1,86 @@
+// Host emulation of the few HIP device facilities strict_scan.hip's kernel uses, for the CPU
+// test of its wave-level logic (tests/test_scan_emulation.py).  Test infrastructure only.
+// One wave = 64 lanes run as stackful coroutines (ucontext) in one thread; every cross-lane
+// operation (shuffles, __any) is a lockstep point: each lane publishes its value and yields,
+// and reads once every lane has published.  Correct for kernels whose cross-lane operations
+// sit in wave-uniform control flow, as the kernel's do.
+#pragma once
+#include <ucontext.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+using std::fabs;
+using std::fma;
+using std::isfinite;
+using std::max;
+using std::min;
+#define __global__
+#define __device__
+#define __host__
+#define __forceinline__ inline
+#define __launch_bounds__(...)
+typedef int hipError_t;
+typedef void* hipStream_t;
+typedef void* hipEvent_t;
+enum { hipSuccess = 0, hipErrorInvalidValue = 1, hipErrorOutOfMemory = 2 };
+struct EmuDim3 {
+  unsigned x = 0, y = 0, z = 0;
+};
+extern EmuDim3 threadIdx, blockIdx;
+extern uint64_t emu_buf[64];
+void emu_yield();
+inline double __builtin_amdgcn_rcp(double x) { return 1.0 / x; }
+template <class T>
+inline T emu_xchg(T v, int src) {
+  uint64_t u = 0;
+  std::memcpy(&u, &v, sizeof(T));
+  emu_buf[threadIdx.x] = u;
+  emu_yield();
+  const uint64_t r = emu_buf[src];
+  emu_yield();
+  T o;
+  std::memcpy(&o, &r, sizeof(T));
+  return o;
+}
+template <class T>
+inline T __shfl_down(T v, int d, int = 64) {
+  const int l = (int)threadIdx.x;
+  return emu_xchg(v, l + d < 64 ? l + d : l);
+}
+template <class T>
+inline T __shfl_up(T v, int d, int = 64) {
+  const int l = (int)threadIdx.x;
+  return emu_xchg(v, l >= d ? l - d : l);
+}
+template <class T>
+inline T __shfl(T v, int s, int = 64) {
+  return emu_xchg(v, s);
+}
+inline bool __any(bool b) {
+  emu_buf[threadIdx.x] = b;
+  emu_yield();
+  bool r = false;
+  for (int i = 0; i < 64; ++i) r |= emu_buf[i] != 0;
+  emu_yield();
+  return r;
+}
+inline int atomicOr(int32_t* p, int v) {
+  const int o = *p;
+  *p |= v;
+  return o;
+}
+inline unsigned long long atomicAdd(unsigned long long* p, unsigned long long v) {
+  const auto o = *p;
+  *p += v;
+  return o;
+}
+inline unsigned long long atomicMax(unsigned long long* p, unsigned long long v) {
+  const auto o = *p;
+  *p = std::max(*p, v);
+  return o;
+}
+#define hipLaunchKernelGGL(...) (void)0
+inline hipError_t hipGetLastError() { return 0; }
+inline hipError_t hipMemsetAsync(void*, int, size_t, hipStream_t) { return 0; }
