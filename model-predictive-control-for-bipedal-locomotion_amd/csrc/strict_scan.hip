@@ -279,22 +279,30 @@ __device__ __forceinline__ void shfl_down_elem(const Elem& e, Elem& o, int d) {
   for (int q = 0; q < 6; ++q) o.J[q] = __shfl_down(e.J[q], d, 64);
 }
 
-// One instance per workgroup (one wave); lane l owns slots [lC, lC + C) ∩ [0, N).
-template <int C>
-__global__ void __launch_bounds__(64) zmpc_strict_scan_kernel(ScanArgs a) {
+// One wave per workgroup holding 64/L instances of L lanes each; lane l of an instance owns
+// slots [lC, lC + C) ∩ [0, N).  The scans stay inside an instance's L lanes; an instance that
+// has converged keeps its working set while the others of its wave iterate (a converged set
+// reproduces itself, so its extra passes change nothing; they are not counted).
+template <int C, int L>
+__global__ void __launch_bounds__(64, 2) zmpc_strict_scan_kernel(ScanArgs a) {
+  static_assert(L == 64 || L == 32 || L == 16, "lanes per instance");
   const int lane = threadIdx.x;
+  const int il = lane & (L - 1);     // lane within the instance
+  const int base = lane & ~(L - 1);  // the instance's first lane
   const int N = a.N;
-  const int64_t w = blockIdx.x;
-  const int64_t b = a.window_mode ? w : (w >> 1);
-  const int axis = a.window_mode ? 0 : (int)(w & 1);
-  const int k0 = lane * C;
+  const int64_t w = (int64_t)blockIdx.x * (64 / L) + lane / L;
+  const bool valid = w < a.ninst;
+  const int64_t wc = valid ? w : 0;  // (a clamped instance for loads; nothing is written)
+  const int64_t b = a.window_mode ? wc : (wc >> 1);
+  const int axis = a.window_mode ? 0 : (int)(wc & 1);
+  const int k0 = il * C;
   double x[3];
   {
     const double* xp = a.window_mode ? a.x0 + b * 3 : a.x0 + (b * 2 + axis) * 3;
     x[0] = xp[0];
     x[1] = xp[1];
     x[2] = xp[2];
-    if (!a.window_mode && lane == 0) {
+    if (!a.window_mode && il == 0 && valid) {
       double* h = a.out + ((b * a.n) * 2 + axis) * 3;  // hist[b, 0, axis, :] = x0
       h[0] = x[0];
       h[1] = x[1];
@@ -311,10 +319,11 @@ __global__ void __launch_bounds__(64) zmpc_strict_scan_kernel(ScanArgs a) {
   int fq = 0;
   unsigned long long passes = 0;
   unsigned itmax = 0;
+  const unsigned long long imask = (L == 64) ? ~0ull : (((1ull << L) - 1) << base);
 
-  for (int64_t i = 0; i < a.nsteps; ++i) {
-    // the window's (z_ref, half-width) of the lane's slots (padding: the last sample)
-    double r[C], h[C];
+  // the window's (z_ref, half-width) of the lane's slots at timestep i (padding: the last
+  // sample); the next timestep's are loaded while this one's passes run
+  auto load_window = [&](int64_t i, double* hi, double* lo) {
 #pragma unroll
     for (int q = 0; q < C; ++q) {
       const int k = min(k0 + q, N - 1);
@@ -326,10 +335,20 @@ __global__ void __launch_bounds__(64) zmpc_strict_scan_kernel(ScanArgs a) {
         if (t > a.n - 1) t = a.n - 1;
         e = b * a.bstride + t * 2 + axis;
       }
-      const double hi = a.zmax[e], lo = a.zmin[e];
-      r[q] = (hi + lo) / 2;  // z_ref (zmp_controller.py:184)
-      h[q] = (hi - lo) / 2;
+      hi[q] = a.zmax[e];
+      lo[q] = a.zmin[e];
     }
+  };
+  double nhi[C], nlo[C];
+  load_window(0, nhi, nlo);
+  for (int64_t i = 0; i < a.nsteps; ++i) {
+    double r[C], h[C];
+#pragma unroll
+    for (int q = 0; q < C; ++q) {
+      r[q] = (nhi[q] + nlo[q]) / 2;  // z_ref (zmp_controller.py:184)
+      h[q] = (nhi[q] - nlo[q]) / 2;
+    }
+    if (i + 1 < a.nsteps) load_window(i + 1, nhi, nlo);
     // η of the state (strict_lq.hip)
     double e0[3];
     {
@@ -340,7 +359,8 @@ __global__ void __launch_bounds__(64) zmpc_strict_scan_kernel(ScanArgs a) {
     }
     double v0 = 0.0;
     int it = 0;
-    bool again = true;
+    bool mine = valid;  // this instance still iterating
+    bool again = __any(mine);
     while (again) {
       // ---- backward: chunk element, suffix scan, V at the chunk's end ------------------------
       Ric v;
@@ -362,10 +382,10 @@ __global__ void __launch_bounds__(64) zmpc_strict_scan_kernel(ScanArgs a) {
           }
         }
 #pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
+        for (int d = 1; d < L; d <<= 1) {
           Elem P;
           shfl_down_elem(E, P, d);
-          if (lane + d < 64) combine(E, P);
+          if (il + d < L) combine(E, P);
         }
         // V at the chunk's end = the right neighbour's suffix (0 past the horizon).  Every lane
         // takes part in the shuffles (a source lane outside the exec mask reads as 0); the last
@@ -376,7 +396,7 @@ __global__ void __launch_bounds__(64) zmpc_strict_scan_kernel(ScanArgs a) {
           for (int q = 0; q < 6; ++q) vv[q] = __shfl_down(E.J[q], 1, 64);
 #pragma unroll
           for (int q = 0; q < 3; ++q) vv[6 + q] = __shfl_down(E.g[q], 1, 64);
-          const bool last = lane == 63;
+          const bool last = il == L - 1;
           v.p00 = last ? 0.0 : vv[0];
           v.p01 = last ? 0.0 : vv[1];
           v.p02 = last ? 0.0 : vv[2];
@@ -388,14 +408,11 @@ __global__ void __launch_bounds__(64) zmpc_strict_scan_kernel(ScanArgs a) {
           v.s2 = last ? 0.0 : vv[8];
         }
       }
-      // ---- the lane's slots: Riccati back from V_end; keep the laws and V_{k+1}'s last column
-      double K0[C], K1[C], K2[C], kf[C], vp02[C], vp12[C], vp22[C], vs2[C];
+      // ---- the lane's slots: Riccati back from V_end, keeping the laws (v ends as V at the
+      // chunk's start)
+      double K0[C], K1[C], K2[C], kf[C];
 #pragma unroll
       for (int q = C - 1; q >= 0; --q) {
-        vp02[q] = v.p02;
-        vp12[q] = v.p12;
-        vp22[q] = v.p22;
-        vs2[q] = v.s2;
         if (k0 + q < N) ric_step(a, v, r[q], h[q], f[q], K0[q], K1[q], K2[q], kf[q]);
         else K0[q] = K1[q] = K2[q] = kf[q] = 0.0;
       }
@@ -424,13 +441,13 @@ __global__ void __launch_bounds__(64) zmpc_strict_scan_kernel(ScanArgs a) {
         }
       }
 #pragma unroll
-      for (int d = 1; d < 64; d <<= 1) {
+      for (int d = 1; d < L; d <<= 1) {
         double Fp[9], pp[3];
 #pragma unroll
         for (int q = 0; q < 9; ++q) Fp[q] = __shfl_up(F[q], d, 64);
 #pragma unroll
         for (int q = 0; q < 3; ++q) pp[q] = __shfl_up(ph[q], d, 64);
-        if (lane >= d) {  // (F, φ) ← (F, φ) ∘ (Fp, pp): the earlier lanes' map first
+        if (il >= d) {  // (F, φ) ← (F, φ) ∘ (Fp, pp): the earlier lanes' map first
           double Fn[9], pn[3];
 #pragma unroll
           for (int i2 = 0; i2 < 3; ++i2) {
@@ -454,42 +471,79 @@ __global__ void __launch_bounds__(64) zmpc_strict_scan_kernel(ScanArgs a) {
 #pragma unroll
         for (int i2 = 0; i2 < 3; ++i2) {
           const double up = __shfl_up(xe[i2], 1, 64);
-          xs[i2] = lane == 0 ? e0[i2] : up;
+          xs[i2] = il == 0 ? e0[i2] : up;
         }
       }
-      // ---- the lane's slots forward: primal check (free), multiplier check (pinned) ----------
-      bool changed = false;
+      // ---- the lane's slots forward: roll out, primal check of the free slots --------------
+      // costate at the chunk's end: λ = ∇V(η) = P η − s at the right neighbour's chunk start
+      // (0 past the horizon: V_N = 0 there, and idle lanes carry it)
+      double lam[3];
+      {
+        double ls[3];
+        ls[0] = fma(v.p00, xs[0], fma(v.p01, xs[1], v.p02 * xs[2])) - v.s0;
+        ls[1] = fma(v.p01, xs[0], fma(v.p11, xs[1], v.p12 * xs[2])) - v.s1;
+        ls[2] = fma(v.p02, xs[0], fma(v.p12, xs[1], v.p22 * xs[2])) - v.s2;
+#pragma unroll
+        for (int i2 = 0; i2 < 3; ++i2) {
+          const double dn = __shfl_down(ls[i2], 1, 64);
+          lam[i2] = il == L - 1 ? 0.0 : dn;
+        }
+      }
+      double wv[C];  // z − r at a free slot, v at a pinned one (strict_lq.hip seg_forward)
+      int np[C];     // a free slot's primal verdict
       const double tol = 1e-13;  // as strict_lq.hip
 #pragma unroll
       for (int q = 0; q < C; ++q) {
+        wv[q] = 0.0;
+        np[q] = 0;
         if (k0 + q < N) {
           double vq, z;
           fwd_step(a, K0[q], K1[q], K2[q], kf[q], xs, vq, z);
-          if (k0 + q == 0) v0 = vq;
+          if (k0 + q == 0 && mine) v0 = vq;
           const double d = z - r[q], ht = h[q] + tol;
-          const int np = (d > ht) ? 1 : ((d < -ht) ? -1 : 0);
-          // pinned: π e + ρ v + λ2_{k+1} = 0, λ_{k+1} = P_{k+1} η_{k+1} − s_{k+1}
-          const double lam2 = fma(vp02[q], xs[0], fma(vp12[q], xs[1], vp22[q] * xs[2])) - vs2[q];
-          const double e = -fma(a.rho, vq, lam2) * a.ipi;
-          const double sg = (double)f[q];
-          const double nu = fma(-sg, h[q], e);
-          const bool rel = sg * nu < -a.tolnu;
-          const int nf = (f[q] == 0) ? np : (rel ? 0 : f[q]);
-          changed |= nf != f[q];
-          f[q] = nf;
+          wv[q] = (f[q] == 0) ? d : vq;
+          np[q] = (d > ht) ? 1 : ((d < -ht) ? -1 : 0);
         }
       }
-      ++it;
-      again = __any(changed);
-      if (again && it >= SC_MAXIT) {
-        fq |= ZMPC_ST_MAXITER;
-        again = false;
+      // ---- costate back through the chunk (strict_lq.hip seg_costate): the pinned slots'
+      // multipliers, dual check, the new working set
+      bool changed = false;
+#pragma unroll
+      for (int q = C - 1; q >= 0; --q) {
+        if (k0 + q < N) {
+          const int fl = f[q];
+          // pinned: π e + ρ v + λ2_{k+1} = 0 (stationarity in v_k)
+          const double e = (fl == 0) ? wv[q] : -fma(a.rho, wv[q], lam[2]) * a.ipi;
+          const double sg = (double)fl;
+          const double nu = fma(-sg, h[q], e);  // e − (t − r): ν / Q at pinned slots
+          const bool rel = sg * nu < -a.tolnu;
+          const int nf = (fl == 0) ? np[q] : (rel ? 0 : fl);
+          changed |= nf != fl;
+          if (mine) f[q] = nf;
+          const double s01 = lam[0] + lam[1];
+          const double s012 = s01 + lam[2];
+          lam[0] = e + lam[0];
+          lam[1] = e + s01;
+          lam[2] = fma(a.gp, e, s012);
+        }
       }
+      // the instance's verdict (its L lanes of the wave's ballot)
+      const bool ich = (__ballot(changed) & imask) != 0;
+      if (mine) {
+        ++it;
+        if (!ich) {
+          mine = false;
+        } else if (it >= SC_MAXIT) {
+          fq |= ZMPC_ST_MAXITER;
+          mine = false;
+        }
+      }
+      again = __any(mine);
     }
     passes += (unsigned long long)it;
     itmax = max(itmax, (unsigned)it);
     // converged: advance in the reference form x⁺ = A x + B u0 (zmp_controller.py:199)
-    const double u0 = __shfl(v0, 0, 64) / a.Tcu;
+    const double u0 = __shfl(v0, base, 64) / a.Tcu;
     double xn[3];
     xn[0] = x[0] + a.T * x[1] + a.T2 * x[2] + a.T3 * u0;
     xn[1] = x[1] + a.T * x[2] + a.T2 * u0;
@@ -499,7 +553,7 @@ __global__ void __launch_bounds__(64) zmpc_strict_scan_kernel(ScanArgs a) {
     x[0] = xn[0];
     x[1] = xn[1];
     x[2] = xn[2];
-    if (lane == 0) {
+    if (il == 0 && valid) {
       double* o = a.window_mode ? a.out + b * 3 : a.out + ((b * a.n + i + 1) * 2 + axis) * 3;
       o[0] = xn[0];
       o[1] = xn[1];
@@ -519,7 +573,7 @@ __global__ void __launch_bounds__(64) zmpc_strict_scan_kernel(ScanArgs a) {
       for (int q = 0; q < C; ++q) f[q] = (k0 + q < N) ? g[q] : 0;
     }
   }
-  if (lane == 0) {
+  if (il == 0 && valid) {
     if (a.status != nullptr) {
       if (a.window_mode)
         a.status[b] = fq;
@@ -559,12 +613,36 @@ void fill(const zmpc_plan* p, ScanArgs& a) {
   a.cnt = p->lqcnt;
 }
 
-hipError_t launch(const zmpc_plan* p, const ScanArgs& a, hipStream_t s) {
-  const dim3 grid((unsigned)a.ninst), blk(64);
+// Lanes per instance: a whole wave while the instances fit the chip's resident waves (the
+// latency of one pass is what counts), 32 beyond (half the waves; the chunks of up to 8 slots
+// keep N ≤ 256 in registers).
+int lanes_per_instance(const zmpc_plan* p, int64_t ninst) {
+  const int64_t resident = (int64_t)(p->cus > 0 ? p->cus : 256) * 4 * 2;  // 2 waves per SIMD
+  return (ninst > resident && p->N <= 256) ? 32 : 64;
+}
+
+hipError_t launch(const zmpc_plan* p, const ScanArgs& a, hipStream_t s, int L) {
+  const dim3 blk(64);
+  if (L == 32) {
+    const dim3 grid((unsigned)((a.ninst + 1) / 2));
+    switch ((p->N + 31) / 32) {
+#define ZMPC_SCASE(CC)                                                        \
+  case CC:                                                                    \
+    hipLaunchKernelGGL((zmpc_strict_scan_kernel<CC, 32>), grid, blk, 0, s, a); \
+    break;
+      ZMPC_SCASE(1) ZMPC_SCASE(2) ZMPC_SCASE(3) ZMPC_SCASE(4) ZMPC_SCASE(5) ZMPC_SCASE(6)
+      ZMPC_SCASE(7) ZMPC_SCASE(8)
+#undef ZMPC_SCASE
+      default:
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
+  const dim3 grid((unsigned)a.ninst);
   switch ((p->N + 63) / 64) {
-#define ZMPC_SCASE(CC)                                                    \
-  case CC:                                                                \
-    hipLaunchKernelGGL(zmpc_strict_scan_kernel<CC>, grid, blk, 0, s, a); \
+#define ZMPC_SCASE(CC)                                                        \
+  case CC:                                                                    \
+    hipLaunchKernelGGL((zmpc_strict_scan_kernel<CC, 64>), grid, blk, 0, s, a); \
     break;
     ZMPC_SCASE(1) ZMPC_SCASE(2) ZMPC_SCASE(3) ZMPC_SCASE(4) ZMPC_SCASE(5) ZMPC_SCASE(6)
     ZMPC_SCASE(7) ZMPC_SCASE(8)
@@ -610,7 +688,7 @@ hipError_t zmpc_launch_rollout_strict_scan(const zmpc_plan* p, int64_t B, int64_
   a.kick_steps = kick_steps;
   a.out = hist;
   a.status = status;
-  return launch(p, a, s);
+  return launch(p, a, s, lanes_per_instance(p, a.ninst));
 }
 
 hipError_t zmpc_launch_step_strict_scan(const zmpc_plan* p, int64_t B, const double* x,
@@ -636,5 +714,5 @@ hipError_t zmpc_launch_step_strict_scan(const zmpc_plan* p, int64_t B, const dou
   a.out = x_next;
   a.status = status;
   a.kick_step = -1;
-  return launch(p, a, s);
+  return launch(p, a, s, lanes_per_instance(p, a.ninst));
 }

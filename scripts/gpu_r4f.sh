@@ -11,8 +11,12 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout
 step pytest $?; tail -1 "$OUT/pytest.log"
 timeout -k 10 500 python scripts/strict_small_batch.py > "$OUT/small_batch.jsonl" 2> "$OUT/small_batch.err"
 step small $?; cat "$OUT/small_batch.jsonl"
-timeout -k 10 300 python bench.py --config 6 --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/bench_c6.json" 2> "$OUT/bench_c6.err"
-step config6 $?; cut -c1-220 "$OUT/bench_c6.json"
+L=model-predictive-control-for-bipedal-locomotion_amd/mpc_bipedal
+for v in base hbase base hbase; do  # Herdt: this build vs the last commit's herdt.hip, alternated
+  if [ $v = base ]; then lib=$PWD/$L/libzmpc.so; else lib=$PWD/$L/ab/libzmpc_$v.so; fi
+  ZMPC_LIB=$lib timeout -k 10 300 python bench.py --config 6 --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/bench_c6_$v.json" 2> "$OUT/bench_c6_$v.err"
+  step "config6 $v" $?; python3 -c "import json; d=json.loads(open('$OUT/bench_c6_$v.json').read().strip().splitlines()[-1]); print('$v', d['ms_per_step'], d['roofline'].get('kernel_ms'), d.get('com_rmse_vs_ref'))"
+done
 # strict LQ kernel A/B of build-time parameters (csrc/Makefile `ab`): segment length, drift
 L=model-predictive-control-for-bipedal-locomotion_amd/mpc_bipedal
 for c in 3 4; do

@@ -66,6 +66,14 @@ inline bool __any(bool b) {
   emu_yield();
   return r;
 }
+inline unsigned long long __ballot(bool b) {
+  emu_buf[threadIdx.x] = b;
+  emu_yield();
+  unsigned long long m = 0;
+  for (int i = 0; i < 64; ++i) m |= (unsigned long long)(emu_buf[i] != 0) << i;
+  emu_yield();
+  return m;
+}
 inline int atomicOr(int32_t* p, int v) {
   const int o = *p;
   *p |= v;

@@ -1,6 +1,6 @@
 // Driver of the host emulation of zmpc_strict_scan_kernel (tests/test_scan_emulation.py): one
 // strict rollout of one walk (both axes) from a binary input file, the history to stdout.
-// Input: int32 N, int64 n, f64 T, h/g, Q, R, zmax[n][2], zmin[n][2], x0[2][3], kick, int64
+// argv[2]: lanes per instance (64, default, or 32).  Input: int32 N, int64 n, f64 T, h/g, Q, R, zmax[n][2], zmin[n][2], x0[2][3], kick, int64
 // kick step (−1: none).  Test infrastructure only.
 #include "hip/hip_runtime.h"
 
@@ -14,25 +14,41 @@ void emu_yield() { swapcontext(&g_lane[g_cur], &g_main); }
 #include "scan_kernel_emu.h"  // generated from csrc/strict_scan.hip (kernel part)
 
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 
 static emu::ScanArgs g_args;
+static int g_L = 64;  // lanes per instance
 static void lane_main() {
-  switch ((g_args.N + 63) / 64) {
-#define EMU_CASE(CC) \
-  case CC:           \
-    emu::zmpc_strict_scan_kernel<CC>(g_args); \
+  if (g_L == 64) {
+    switch ((g_args.N + 63) / 64) {
+#define EMU_CASE(CC)                                  \
+  case CC:                                            \
+    emu::zmpc_strict_scan_kernel<CC, 64>(g_args); \
     break;
-    EMU_CASE(1) EMU_CASE(2) EMU_CASE(3) EMU_CASE(4) EMU_CASE(5) EMU_CASE(6) EMU_CASE(7) EMU_CASE(8)
+      EMU_CASE(1) EMU_CASE(2) EMU_CASE(3) EMU_CASE(4) EMU_CASE(5) EMU_CASE(6) EMU_CASE(7) EMU_CASE(8)
 #undef EMU_CASE
-    default:
-      break;
+      default:
+        break;
+    }
+  } else {
+    switch ((g_args.N + 31) / 32) {
+#define EMU_CASE(CC)                                  \
+  case CC:                                            \
+    emu::zmpc_strict_scan_kernel<CC, 32>(g_args); \
+    break;
+      EMU_CASE(1) EMU_CASE(2) EMU_CASE(3) EMU_CASE(4) EMU_CASE(5) EMU_CASE(6) EMU_CASE(7) EMU_CASE(8)
+#undef EMU_CASE
+      default:
+        break;
+    }
   }
   g_done[g_cur] = true;
 }
 
 int main(int argc, char** argv) {
   if (argc < 2) return 2;
+  if (argc > 2) g_L = atoi(argv[2]);
   FILE* f = fopen(argv[1], "rb");
   if (!f) return 2;
   int N = 0;
@@ -85,7 +101,8 @@ int main(int argc, char** argv) {
   a.status = &status;
   a.cnt = nullptr;
   std::vector<char> stacks((size_t)64 << 20);
-  for (unsigned w = 0; w < 2; ++w) {  // one wave per (walk, axis) instance
+  const unsigned waves = g_L == 64 ? 2 : 1;  // the walk's two (walk, axis) instances
+  for (unsigned w = 0; w < waves; ++w) {
     blockIdx.x = w;
     for (int l = 0; l < 64; ++l) {
       getcontext(&g_lane[l]);

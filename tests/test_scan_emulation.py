@@ -35,7 +35,7 @@ def emulator(tmp_path_factory):
     return d, exe
 
 
-def _run(emulator, N, x0, kick, kstep):
+def _run(emulator, N, x0, kick, kstep, lanes=64):
     d, exe = emulator
     s = golden("strict_ref.npz")
     zx, zn = s[f"n{N}_zmax"], s[f"n{N}_zmin"]
@@ -47,15 +47,18 @@ def _run(emulator, N, x0, kick, kstep):
         f.write(np.ascontiguousarray(zn, np.float64).tobytes())
         f.write(np.asarray(x0, np.float64).reshape(6).tobytes())
         f.write(struct.pack("<dq", kick, kstep))
-    r = subprocess.run([str(exe), str(inp)], capture_output=True, check=True, timeout=600)
+    r = subprocess.run([str(exe), str(inp), str(lanes)], capture_output=True, check=True,
+                       timeout=600)
     assert r.stderr.decode().strip() == "status 0"
     return np.frombuffer(r.stdout, np.float64).reshape(n, 2, 3), s, n
 
 
-@pytest.mark.parametrize("N,F", ((64, 800), (150, 400)))
-def test_scan_kernel_emulated_kicked_walk(emulator, N, F):
+@pytest.mark.parametrize("N,F,lanes", ((64, 800, 64), (150, 400, 64), (150, 800, 32)))
+def test_scan_kernel_emulated_kicked_walk(emulator, N, F, lanes):
+    """Both lane counts per instance: a whole wave, and two instances (the walk's two axes) per
+    wave of 32 lanes each."""
     n = len(golden("strict_ref.npz")[f"n{N}_zmax"])
-    h, s, _ = _run(emulator, N, np.zeros(6), (1.5 / N) * F / 40.0, n // 2)
+    h, s, _ = _run(emulator, N, np.zeros(6), (1.5 / N) * F / 40.0, n // 2, lanes)
     assert np.abs(h[:, :, 0] - s[f"n{N}_F{F}_com"]).max() <= 1e-12
 
 
