@@ -553,7 +553,7 @@ __global__ void __launch_bounds__(64 * G, 2)
   // RUNS: the run holding the window's last slot of the last segment (sweep A starts there)
   // and the one holding its first slot (sweep B), advanced as the lane's timestep moves
   int ra = 0, rb = 0;
-  if constexpr (RUNS) {
+  if (RUNS && valid) {  // (positions past B may lie past the staged groups: never read)
     const int tA = (int)a.toff + a.NS * S - 1, tB = (int)a.toff;
     while (L.rt[(ra + 1) * 64 + lane] <= tA) ++ra;
     while (L.rt[(rb + 1) * 64 + lane] <= tB) ++rb;
