@@ -1395,7 +1395,9 @@ struct WideGeom {
 
 bool wide_geom(int N, int64_t n, WideGeom* g) {
   const int64_t ns = n - 1;
-  if (ns <= 64 * 8 || ns > 64 * 8 * 8) return false;
+  // (449..512 timesteps: the single-pass split kernel's CW = 8 runs 1.7× slower per walk than
+  // its CW = 7, profiles/r4/r4hp_*; the wide kernel takes them at CW = 4 per wave pair)
+  if (ns <= 64 * 7 || ns > 64 * 8 * 8) return false;
   g->w = ns <= 64 * 8 * 2 ? 2 : (ns <= 64 * 8 * 4 ? 4 : 8);
   g->cw = (int)((ns + 64 * g->w - 1) / (64 * g->w));
   g->kc = (N + g->cw - 1) / g->cw * g->cw;
@@ -1792,7 +1794,11 @@ hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, con
     launch_chunk(s, a, p->N);
     return hipGetLastError();
   }
-  if (g.passes > 1) {
+  const bool generic = p->opt[ZMPC_OPT_ROLLOUT_KERNEL] == 1;
+  // per-walk bounds whose single pass would run at CW = 8 take the wide kernel (wide_geom)
+  const bool wide8 = g.passes == 1 && g.cw == 8 && bstride != 0 && !generic &&
+                     wide_geom(p->N, n, &wg);
+  if (g.passes > 1 || wide8) {
     RolloutArgs q = a;
     q.kc = wg.kc;
     q.lz = wg.lz;
@@ -1831,7 +1837,7 @@ hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, con
     else                                                \
       launch_wide<C, W, 0>(s, q, lds_w, B, p->cus);     \
     break;
-      ZMPC_WCASE(2, 5) ZMPC_WCASE(2, 6) ZMPC_WCASE(2, 7) ZMPC_WCASE(2, 8)
+      ZMPC_WCASE(2, 4) ZMPC_WCASE(2, 5) ZMPC_WCASE(2, 6) ZMPC_WCASE(2, 7) ZMPC_WCASE(2, 8)
       ZMPC_WCASE(4, 5) ZMPC_WCASE(4, 6) ZMPC_WCASE(4, 7) ZMPC_WCASE(4, 8)
       ZMPC_WCASE(8, 5) ZMPC_WCASE(8, 6) ZMPC_WCASE(8, 7) ZMPC_WCASE(8, 8)
 #undef ZMPC_WCASE
@@ -1840,7 +1846,6 @@ hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, con
     }
     return hipGetLastError();
   }
-  const bool generic = p->opt[ZMPC_OPT_ROLLOUT_KERNEL] == 1;
   // shared CoP (bounds stride 0) with a single-pass geometry: f once per launch
   double* fsh = nullptr;
   if (bstride == 0 && !generic && 6 * (size_t)n * sizeof(double) <= 64 * 1024) {

@@ -1049,8 +1049,10 @@ static hipError_t launch_strict(const zmpc_plan* p, StrictArgs a, hipStream_t s,
 // walk 27.6 ms vs the LQ kernel's 29.0, 8 walks 92.8 vs 46.4 — its passes are long when a
 // kicked walk pins many slots).
 // Option 4 / auto at up to kScanMaxInst instances: the parallel-in-time kernel of
-// strict_scan.hip (one instance per wave, the horizon over the lanes).
-constexpr int64_t kScanMaxInst = 4096;
+// strict_scan.hip (one instance per wave, the horizon over the lanes).  Crossover measured at
+// N = 150, n = 420 (profiles/r4/r4h_crossover.jsonl): 4096 walks 19.9 vs 55.2 ms (LQ), 8192
+// walks 35.6 vs 56.8, 16384 walks 65.2 vs 57.8 — the LQ kernel wins from ≈14 000 walks.
+constexpr int64_t kScanMaxInst = 24576;
 enum { kTile = 1, kWave = 2, kLq = 3, kScan = 4 };
 
 static int strict_mode(const zmpc_plan* p, int64_t ninst) {

@@ -406,9 +406,10 @@ def test_rollout_kernel_variants_agree():
     """The default single-pass kernels (split per axis: one walk per workgroup, the fast-FIR or
     sparse correlation; persistent for even chunk widths) and the cross-check kernel (one wave
     per walk, direct correlation: ZMPC_OPT_ROLLOUT_KERNEL = 1) agree, at an odd (n = 420: 7)
-    and an even (n = 360: 6) chunk width, with per-walk and shared CoP."""
-    for Nn, n_cut in ((150, None), (150, 360)):
-        zmax, zmin, x0, F, dt = synthetic_batch(4133, Nn)
+    and an even (n = 360: 6) chunk width, and at n = 480 (chunk width 8: per-walk bounds take
+    the wide kernel), with per-walk and shared CoP."""
+    for Nn, n_cut in ((150, None), (150, 360), (512, 480)):
+        zmax, zmin, x0, F, dt = synthetic_batch(4133 if Nn == 150 else 1031, Nn)
         if n_cut:
             zmax, zmin = zmax[:, :n_cut], zmin[:, :n_cut]
         n = zmax.shape[1]
@@ -886,10 +887,11 @@ def test_strict_solvers_vs_reference(solver):
             plan(600, strict=True).set_option("strict_solver", solver)
 
 
-@pytest.mark.parametrize("B,auto", ((2, 4), (300, 4), (2100, 3)))
+@pytest.mark.parametrize("B,auto", ((2, 4), (300, 4), (2100, 4), (12300, 3)))
 def test_strict_small_and_large_batch_paths_agree(B, auto):
     """The automatic choice (ZMPC_OPT_STRICT_SOLVER = 0) takes the parallel-in-time kernel up to
-    4096 instances and the LQ kernel beyond; on config-3 style batches the small-batch kernels
+    24576 instances (whole waves per instance up to the resident waves, 32 lanes beyond) and the
+    LQ kernel beyond; on config-3 style batches the small-batch kernels
     (forced) and the LQ kernel give the same histories to rounding, and the automatic one equals
     the chosen kernel's bitwise."""
     zmax, zmin, x0, F, dt = synthetic_batch(B, 150, seed=41)
