@@ -139,6 +139,22 @@ struct ZrLayout {
   __host__ __device__ static constexpr int idx(int t) { return t + kPad * (t / CW); }
 };
 
+// History staging of the split kernels: row 0 the initial state, row m + 1 the state after
+// step m (6 doubles: both axes), written by the lane owning step m.  For even CW the lanes'
+// rows are CW·48 bytes apart, a multiple of 128 B, so the 16 lanes of a ds_write_b64 group hit
+// one or two banks (16-way at CW = 8); two pad doubles after every CW rows spread them over
+// eight bank pairs (2-way, as odd CW).  The copy-out skips the pads.
+template <int CW>
+struct HistLayout {
+  static constexpr int kPad = (CW % 2 == 0) ? 2 : 0;  // doubles after every CW step rows
+  __host__ __device__ static constexpr int row(int r) {  // first double of staged row r
+    return r * 6 + (r >= 1 ? kPad * ((r - 1) / CW) : 0);
+  }
+  __host__ __device__ static constexpr size_t doubles(int n) {
+    return (size_t)n * 6 + (size_t)kPad * ((n + CW - 1) / CW);
+  }
+};
+
 struct RolloutGeom {
   int cw, passes, kc, lz, lzp, nf;
   int kfm;  // fast-FIR steps (odd CW; axis_correlate_ffa), 0 otherwise
@@ -822,7 +838,7 @@ __device__ __forceinline__ void split_walk(const RolloutArgs& a, int64_t b, doub
       double xn[3];
       lipm_step(lc, x, u, xn);
       if (m == kick_step) xn[1] -= kk;  // force kick (zmp_controller.py:90,105-106)
-      double* o = stage + (m + 1) * 6 + 3 * axis;
+      double* o = stage + HistLayout<CW>::row(m + 1) + 3 * axis;
       o[0] = xn[0];
       o[1] = xn[1];
       o[2] = xn[2];
@@ -846,14 +862,31 @@ __device__ __forceinline__ void split_walk(const RolloutArgs& a, int64_t b, doub
     // written once and never re-read here: non-temporal stores (config 4 unconstrained
     // 0.547 → 0.497 ms in an A/B on one box; config 2 unchanged)
     int e = tid;
-    for (; e + 3 * 128 < ne; e += 4 * 128) {
-      const double2 v0 = src[e], v1 = src[e + 128], v2 = src[e + 256], v3 = src[e + 384];
-      st_nt2(&dst[e], v0);
-      st_nt2(&dst[e + 128], v1);
-      st_nt2(&dst[e + 256], v2);
-      st_nt2(&dst[e + 384], v3);
+    if constexpr (HistLayout<CW>::kPad == 0) {
+      for (; e + 3 * 128 < ne; e += 4 * 128) {
+        const double2 v0 = src[e], v1 = src[e + 128], v2 = src[e + 256], v3 = src[e + 384];
+        st_nt2(&dst[e], v0);
+        st_nt2(&dst[e + 128], v1);
+        st_nt2(&dst[e + 256], v2);
+        st_nt2(&dst[e + 384], v3);
+      }
+      for (; e < ne; e += 128) st_nt2(&dst[e], src[e]);
+    } else {
+      // element e (a double2) of row r = e / 3 sits behind (r − 1) / CW pads of one double2
+      auto at = [](int e2) {
+        const int r = e2 / 3;
+        return e2 + (r >= 1 ? (r - 1) / CW : 0) * (HistLayout<CW>::kPad / 2);
+      };
+      for (; e + 3 * 128 < ne; e += 4 * 128) {
+        const double2 v0 = src[at(e)], v1 = src[at(e + 128)], v2 = src[at(e + 256)],
+                      v3 = src[at(e + 384)];
+        st_nt2(&dst[e], v0);
+        st_nt2(&dst[e + 128], v1);
+        st_nt2(&dst[e + 256], v2);
+        st_nt2(&dst[e + 384], v3);
+      }
+      for (; e < ne; e += 128) st_nt2(&dst[e], src[at(e)]);
     }
-    for (; e < ne; e += 128) st_nt2(&dst[e], src[e]);
     if constexpr (PM) __builtin_amdgcn_s_setprio(0);
   }
   if (a.status != nullptr && tid == 0) a.status[b] = flag[0] | flag[1];
@@ -1393,6 +1426,11 @@ struct WideGeom {
   int w, cw, kc, lz, lzp;
 };
 
+#ifndef ZMPC_WIDE8  // (A/B builds only)
+#define ZMPC_WIDE8 0
+#endif
+constexpr bool kWide8 = ZMPC_WIDE8 != 0;
+
 bool wide_geom(int N, int64_t n, WideGeom* g) {
   const int64_t ns = n - 1;
   // (449..512 timesteps: the single-pass split kernel's CW = 8 runs 1.7× slower per walk than
@@ -1691,7 +1729,7 @@ template <int CW>
 void launch_unc(const RolloutGeom& g, size_t lds, hipStream_t s, RolloutArgs a, int cus,
                 bool generic) {
   const size_t lds_axis = lds - (size_t)a.kcp * sizeof(double);  // no staged gain row
-  size_t lds_split = std::max<size_t>(lds_axis, 6 * (size_t)a.n * sizeof(double));
+  size_t lds_split = std::max<size_t>(lds_axis, HistLayout<CW>::doubles(a.n) * sizeof(double));
   // the sparse-difference correlation stages the plan's suffix sums behind the z_ref areas
   const size_t lds_sparse = std::max(lds_axis + (size_t)ksum_rows(a.hN) * sizeof(double),
                                      lds_split);
@@ -1702,7 +1740,7 @@ void launch_unc(const RolloutGeom& g, size_t lds, hipStream_t s, RolloutArgs a, 
   if (a.fsh != nullptr) {
     // shared CoP, f precomputed: scan, replay and the history stores only
     hipLaunchKernelGGL((zmpc_rollout_unc_splitd_kernel<CW, true>), dim3((unsigned)a.B),
-                       dim3(128), 6 * (size_t)a.n * sizeof(double), s, a);
+                       dim3(128), HistLayout<CW>::doubles(a.n) * sizeof(double), s, a);
     return;
   }
   if (generic || lds_split > 64 * 1024) {
@@ -1796,7 +1834,7 @@ hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, con
   }
   const bool generic = p->opt[ZMPC_OPT_ROLLOUT_KERNEL] == 1;
   // per-walk bounds whose single pass would run at CW = 8 take the wide kernel (wide_geom)
-  const bool wide8 = g.passes == 1 && g.cw == 8 && bstride != 0 && !generic &&
+  const bool wide8 = kWide8 && g.passes == 1 && g.cw == 8 && bstride != 0 && !generic &&
                      wide_geom(p->N, n, &wg);
   if (g.passes > 1 || wide8) {
     RolloutArgs q = a;
@@ -1848,7 +1886,7 @@ hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, con
   }
   // shared CoP (bounds stride 0) with a single-pass geometry: f once per launch
   double* fsh = nullptr;
-  if (bstride == 0 && !generic && 6 * (size_t)n * sizeof(double) <= 64 * 1024) {
+  if (bstride == 0 && !generic && (6 * (size_t)n + 2 * (size_t)n) * sizeof(double) <= 64 * 1024) {
     a.fstride = ((64 * g.cw) + 63) & ~63;  // every lane's CW values, padded
     hipError_t e = hipMallocAsync((void**)&fsh, 2 * (size_t)a.fstride * sizeof(double), s);
     if (e != hipSuccess) {
