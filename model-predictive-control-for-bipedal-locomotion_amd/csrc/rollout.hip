@@ -1366,8 +1366,12 @@ __global__ void __launch_bounds__(128 * W, E == 4 ? 6 : 4) zmpc_rollout_unc_wide
     xs0[i] = (lane == 0) ? xs[i] : p;
   }
   // ---- 4. replay (reference form) into the staging rows, coalesced copy-out per round --------
+  // staging rows padded as the split kernels' (HistLayout: two doubles after every CW local
+  // rows, even CW), so the lanes' ds_write rows are not 128 B multiples apart
   double* stage = smem;
-  const int rows_per_round = (2 * a.lzp) / 6;
+  constexpr int HP = HistLayout<CW>::kPad;
+  const int rows_per_round = (2 * a.lzp) * CW / (6 * CW + HP);
+  auto srow = [](int lr) { return lr * 6 + HP * (lr / CW); };
   double* hb = a.hist + b * (int64_t)n * 6;
   double x[3];
   for (int r0 = 0; r0 < n; r0 += rows_per_round) {
@@ -1389,7 +1393,7 @@ __global__ void __launch_bounds__(128 * W, E == 4 ? 6 : 4) zmpc_rollout_unc_wide
         if (m == kick_step) xn[1] -= kk;
         const int row = m + 1;
         if (row >= r0 && row < r1) {
-          double* o = stage + (row - r0) * 6 + 3 * axis;
+          double* o = stage + srow(row - r0) + 3 * axis;
           o[0] = xn[0];
           o[1] = xn[1];
           o[2] = xn[2];
@@ -1403,7 +1407,8 @@ __global__ void __launch_bounds__(128 * W, E == 4 ? 6 : 4) zmpc_rollout_unc_wide
       const int nd2 = (r1 - r0) * 3;
       const double2* src = reinterpret_cast<const double2*>(stage);
       double2* dst = reinterpret_cast<double2*>(hb + (int64_t)r0 * 6);
-      for (int e = tid; e < nd2; e += NT) st_nt2(&dst[e], src[e]);  // written once
+      for (int e = tid; e < nd2; e += NT)  // written once
+        st_nt2(&dst[e], src[e + (HP / 2) * ((e / 3) / CW)]);
     }
     __syncthreads();
   }
