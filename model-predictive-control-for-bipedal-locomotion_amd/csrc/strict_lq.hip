@@ -61,6 +61,7 @@ constexpr int LQ_MAXIT = 64;  // active-set pass cap (as strict.hip)
 #ifndef ZMPC_LQ_DRIFT
 #define ZMPC_LQ_DRIFT 4
 #endif
+
 constexpr int LQ_S = ZMPC_LQ_S;  // Riccati steps per checkpoint segment
 constexpr int LQ_DRIFT = ZMPC_LQ_DRIFT;  // timesteps a lane may run ahead of its wave's slowest lane
                               // (round 3, profiles/r3u/, r3drift/: 0/1/2/4/8 → 104.5/94.8/92.5/
@@ -163,7 +164,8 @@ struct Lane {
   const double2* hl;  // wave's staged (z_ref, half-width) rows (uniform)
   const double2* rs;  // RUNS: wave's run table (uniform)
   const int* rt;
-  int lane;
+  int lane;  // the wave lane (slot flags in LDS)
+  int col;   // the lane's column in the staged tables (its walk position mod 64)
 };
 
 // RUNS: a lane's cursor on its walk's run list while a sweep moves through the window: the
@@ -181,13 +183,13 @@ struct RunCursor {
 __device__ __forceinline__ RunCursor run_fwd(const Lane& L, int ci) {
   RunCursor c;
   c.ci = ci;
-  const double2 v = L.rs[ci * 64 + L.lane], w = L.rs[(ci + 1) * 64 + L.lane];
+  const double2 v = L.rs[ci * 64 + L.col], w = L.rs[(ci + 1) * 64 + L.col];
   c.r = v.x;
   c.h = v.y;
   c.nr = w.x;
   c.nh = w.y;
-  c.e1 = L.rt[(ci + 1) * 64 + L.lane];
-  c.e2 = L.rt[(ci + 2) * 64 + L.lane];
+  c.e1 = L.rt[(ci + 1) * 64 + L.col];
+  c.e2 = L.rt[(ci + 2) * 64 + L.col];
   return c;
 }
 
@@ -195,13 +197,13 @@ __device__ __forceinline__ RunCursor run_bwd(const Lane& L, int ci) {
   RunCursor c;
   c.ci = ci;
   const int pi = max(ci - 1, 0);
-  const double2 v = L.rs[ci * 64 + L.lane], w = L.rs[pi * 64 + L.lane];
+  const double2 v = L.rs[ci * 64 + L.col], w = L.rs[pi * 64 + L.col];
   c.r = v.x;
   c.h = v.y;
   c.nr = w.x;
   c.nh = w.y;
-  c.e1 = L.rt[ci * 64 + L.lane];
-  c.e2 = L.rt[pi * 64 + L.lane];
+  c.e1 = L.rt[ci * 64 + L.col];
+  c.e2 = L.rt[pi * 64 + L.col];
   return c;
 }
 
@@ -217,10 +219,10 @@ __device__ __forceinline__ void seg_runs(const Lane& L, int t0, RunCursor& c, do
         c.r = c.nr;
         c.h = c.nh;
         c.e1 = c.e2;
-        const double2 w = L.rs[(c.ci + 1) * 64 + L.lane];
+        const double2 w = L.rs[(c.ci + 1) * 64 + L.col];
         c.nr = w.x;
         c.nh = w.y;
-        c.e2 = L.rt[(c.ci + 2) * 64 + L.lane];
+        c.e2 = L.rt[(c.ci + 2) * 64 + L.col];
       }
       r[q] = c.r;
       h[q] = c.h;
@@ -234,10 +236,10 @@ __device__ __forceinline__ void seg_runs(const Lane& L, int t0, RunCursor& c, do
         c.h = c.nh;
         c.e1 = c.e2;
         const int pi = max(c.ci - 1, 0);
-        const double2 w = L.rs[pi * 64 + L.lane];
+        const double2 w = L.rs[pi * 64 + L.col];
         c.nr = w.x;
         c.nh = w.y;
-        c.e2 = L.rt[pi * 64 + L.lane];
+        c.e2 = L.rt[pi * 64 + L.col];
       }
       r[q] = c.r;
       h[q] = c.h;
@@ -266,7 +268,7 @@ __device__ __forceinline__ void seg_load(const LqArgs& a, int j, const Lane& L, 
   const double2* hp = L.hl + row0 * 64;
 #pragma unroll
   for (int q = 0; q < S; ++q) {
-    const double2 v = hp[q * 64 + L.lane];
+    const double2 v = hp[q * 64 + L.col];
     in.r[q] = v.x;
     in.h[q] = v.y;
     if (FLAGS) in.f[q] = fl.get(j * S + q, L.lane);
@@ -509,7 +511,10 @@ __device__ __forceinline__ void ck_load_s(const CkIO<NT>& io, const double* ck, 
 // four 64-walk groups, so each SIMD (waves w and w + 4 under the round-robin placement) holds
 // one wave of each axis — the y axis carries nearly all of the active-set work, and an
 // axis-pure SIMD would idle once its x waves are done (config 3: 117 → 98 ms, round 1).  Longer
-// horizons (slot flags of G waves beyond LDS) run G = 4 (x/y = wave parity), 2 or 1.
+// horizons (slot flags of G waves beyond LDS) run G = 4 (x/y = wave parity), 2 or 1.  (Round 4:
+// waves of 32 walks × both axes, so that every SIMD keeps two y-carrying waves to the end, are
+// slower — config 3 87.0 vs 64.9 ms: the x lanes then run the working-set form up to the wave's
+// last pinned slot, 0.76 of the pass-slots instead of 0.48, profiles/r4/r4l_*.)
 template <int S, int G, bool NT, bool RUNS>
 __global__ void __launch_bounds__(64 * G, 2)
     zmpc_strict_lq_kernel(LqArgs a, const double* __restrict__ tab) {
@@ -523,25 +528,27 @@ __global__ void __launch_bounds__(64 * G, 2)
   double* ck = a.ck + (size_t)gw * a.NS * kCkStride;
   const CkIO<NT> io{};
   int axis;
-  int64_t b0;
+  int64_t pos;  // the lane's walk position (order.hip's kick order, or the walk itself)
   if (a.window_mode) {
     axis = 0;
-    b0 = gw * 64;
+    pos = gw * 64 + lane;
   } else if (G == 8) {
     axis = wave >> 2;
-    b0 = ((int64_t)blockIdx.x * 4 + (wave & 3)) * 64;
+    pos = ((int64_t)blockIdx.x * 4 + (wave & 3)) * 64 + lane;
   } else {
     axis = (int)(gw & 1);
-    b0 = (gw >> 1) * 64;
+    pos = (gw >> 1) * 64 + lane;
   }
-  // lane position b0 + lane runs walk b (the kick order of order.hip, or the identity); the
-  // staged bounds follow the positions, everything per walk (x0, kick, history, status) b
-  const bool valid = b0 + lane < a.B;
-  const int64_t b = (valid && a.perm) ? (int64_t)a.perm[b0 + lane] : b0 + lane;
+  // lane position pos runs walk b (the kick order of order.hip, or the identity); the staged
+  // bounds follow the positions (table (axis, pos / 64), column pos % 64), everything per walk
+  // (x0, kick, history, status) b
+  const bool valid = pos < a.B;
+  const int64_t b = (valid && a.perm) ? (int64_t)a.perm[pos] : pos;
   Lane L;
   L.lane = lane;
+  L.col = (int)(pos & 63);
   {
-    const int64_t g = a.shared ? 0 : (b0 >> 6);
+    const int64_t g = a.shared ? 0 : (pos >> 6);
     if constexpr (RUNS) {
       const int64_t off = ((int64_t)axis * a.groups + g) * a.rstride;
       L.rs = a.rs + off;
@@ -555,8 +562,8 @@ __global__ void __launch_bounds__(64 * G, 2)
   int ra = 0, rb = 0;
   if (RUNS && valid) {  // (positions past B may lie past the staged groups: never read)
     const int tA = (int)a.toff + a.NS * S - 1, tB = (int)a.toff;
-    while (L.rt[(ra + 1) * 64 + lane] <= tA) ++ra;
-    while (L.rt[(rb + 1) * 64 + lane] <= tB) ++rb;
+    while (L.rt[(ra + 1) * 64 + L.col] <= tA) ++ra;
+    while (L.rt[(rb + 1) * 64 + L.col] <= tB) ++rb;
   }
   const int jfull = N / S;  // segments [0, jfull) are full
   for (int k = 0; k < fbytes; ++k) fl.p[k * 64 + lane] = 0;
@@ -721,8 +728,8 @@ __global__ void __launch_bounds__(64 * G, 2)
         it = 0;
         if constexpr (RUNS) {
           const int tA = (int)(i + a.toff) + a.NS * S - 1, tB = (int)(i + a.toff);
-          if (L.rt[(ra + 1) * 64 + lane] <= tA) ++ra;  // one slot per timestep: one run at most
-          if (L.rt[(rb + 1) * 64 + lane] <= tB) ++rb;
+          if (L.rt[(ra + 1) * 64 + L.col] <= tA) ++ra;  // one slot per timestep: one run at most
+          if (L.rt[(rb + 1) * 64 + L.col] <= tB) ++rb;
         }
         if (i < a.nsteps) {
           // warm start: the converged set shifted one slot towards the present (slot N−1
