@@ -142,16 +142,19 @@ struct ZrLayout {
 // History staging of the split kernels: row 0 the initial state, row m + 1 the state after
 // step m (6 doubles: both axes), written by the lane owning step m.  For even CW the lanes'
 // rows are CW·48 bytes apart, a multiple of 128 B, so the 16 lanes of a ds_write_b64 group hit
-// one or two banks (16-way at CW = 8); two pad doubles after every CW rows spread them over
-// eight bank pairs (2-way, as odd CW).  The copy-out skips the pads.
+// one or two banks (16-way at CW = 8); two pad doubles after every 2·CW rows (every second
+// lane) spread them over eight bank pairs (2-way, as odd CW) for CW = 2..8, at 2 % more LDS
+// (after every CW rows the same 2-way costs twice the pad, which at n = 476 took one of the seven
+// workgroups a CU holds).  The copy-out skips the pads.
 template <int CW>
 struct HistLayout {
-  static constexpr int kPad = (CW % 2 == 0) ? 2 : 0;  // doubles after every CW step rows
+  static constexpr int kPad = (CW % 2 == 0) ? 2 : 0;  // doubles after every 2·CW step rows
+  static constexpr int kSpan = 2 * CW;
   __host__ __device__ static constexpr int row(int r) {  // first double of staged row r
-    return r * 6 + (r >= 1 ? kPad * ((r - 1) / CW) : 0);
+    return r * 6 + (r >= 1 ? kPad * ((r - 1) / kSpan) : 0);
   }
   __host__ __device__ static constexpr size_t doubles(int n) {
-    return (size_t)n * 6 + (size_t)kPad * ((n + CW - 1) / CW);
+    return (size_t)n * 6 + (size_t)kPad * ((n + kSpan - 1) / kSpan);
   }
 };
 
@@ -872,10 +875,10 @@ __device__ __forceinline__ void split_walk(const RolloutArgs& a, int64_t b, doub
       }
       for (; e < ne; e += 128) st_nt2(&dst[e], src[e]);
     } else {
-      // element e (a double2) of row r = e / 3 sits behind (r − 1) / CW pads of one double2
+      // element e (a double2) of row r = e / 3 sits behind (r − 1) / (2·CW) pads of one double2
       auto at = [](int e2) {
         const int r = e2 / 3;
-        return e2 + (r >= 1 ? (r - 1) / CW : 0) * (HistLayout<CW>::kPad / 2);
+        return e2 + (r >= 1 ? (r - 1) / HistLayout<CW>::kSpan : 0) * (HistLayout<CW>::kPad / 2);
       };
       for (; e + 3 * 128 < ne; e += 4 * 128) {
         const double2 v0 = src[at(e)], v1 = src[at(e + 128)], v2 = src[at(e + 256)],
@@ -1370,8 +1373,9 @@ __global__ void __launch_bounds__(128 * W, E == 4 ? 6 : 4) zmpc_rollout_unc_wide
   // rows, even CW), so the lanes' ds_write rows are not 128 B multiples apart
   double* stage = smem;
   constexpr int HP = HistLayout<CW>::kPad;
-  const int rows_per_round = (2 * a.lzp) * CW / (6 * CW + HP);
-  auto srow = [](int lr) { return lr * 6 + HP * (lr / CW); };
+  constexpr int HS = HistLayout<CW>::kSpan;
+  const int rows_per_round = (2 * a.lzp) * HS / (6 * HS + HP);
+  auto srow = [](int lr) { return lr * 6 + HP * (lr / HS); };
   double* hb = a.hist + b * (int64_t)n * 6;
   double x[3];
   for (int r0 = 0; r0 < n; r0 += rows_per_round) {
@@ -1408,7 +1412,7 @@ __global__ void __launch_bounds__(128 * W, E == 4 ? 6 : 4) zmpc_rollout_unc_wide
       const double2* src = reinterpret_cast<const double2*>(stage);
       double2* dst = reinterpret_cast<double2*>(hb + (int64_t)r0 * 6);
       for (int e = tid; e < nd2; e += NT)  // written once
-        st_nt2(&dst[e], src[e + (HP / 2) * ((e / 3) / CW)]);
+        st_nt2(&dst[e], src[e + (HP / 2) * ((e / 3) / HS)]);
     }
     __syncthreads();
   }
