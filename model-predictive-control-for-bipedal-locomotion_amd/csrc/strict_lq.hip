@@ -583,6 +583,9 @@ __global__ void __launch_bounds__(64 * G, 2)
   }
   int fq = 0;
   unsigned long long n_wave_pass = 0, n_lane_pass = 0, n_ws_slots = 0;
+#ifdef ZMPC_DIAG
+  unsigned long long n_sb_ws = 0, n_sb_free = 0;
+#endif
   const int64_t kstep =
       (!a.window_mode && axis == 1 && a.kick != nullptr && valid)
           ? (a.kick_steps ? a.kick_steps[b] : a.kick_step)
@@ -679,7 +682,14 @@ __global__ void __launch_bounds__(64 * G, 2)
           else
             seg_load<S, true>(a, j, L, i, fl, cur);
           ck_load(io, ck, j, v, lane);
-          // (a free-segment form here — free steps, no costate — spills at 256 VGPRs)
+#ifdef ZMPC_DIAG
+          ++n_sb_ws;  // diagnostics: sweep-B working-set segments, and those no lane pins
+          if (seg_free(cur)) ++n_sb_free;
+#endif
+          // (43 % of these segments have no pinned slot in any lane taking part, config 3,
+          // diagnostics build; a free form for them — ric_free, forward, primal verdicts, no
+          // costate — spills at 256 VGPRs: 74.9 vs 65.0 ms, and 66.7 ms at S = 6,
+          // profiles/r4/r4n/)
           if (j < jfull) {
             seg_sweep_b<S, true>(a, j, v, cur, g, xs, u0, changed, kl, fl, lane);
           } else {
@@ -768,6 +778,10 @@ __global__ void __launch_bounds__(64 * G, 2)
       atomicAdd(a.cnt + 1, n_lane_pass);
       atomicAdd(a.cnt + 2, n_ws_slots);
       if (gw == 0) atomicAdd(a.cnt + 3, 1ull);
+#ifdef ZMPC_DIAG  // (the Herdt counter slots [6], [7], unused by a strict launch)
+      atomicAdd(a.cnt + 6, n_sb_ws);
+      atomicAdd(a.cnt + 7, n_sb_free);
+#endif
       atomicMax(a.cnt + 8, (unsigned long long)itmax);
     }
   }
