@@ -909,6 +909,32 @@ def test_strict_small_and_large_batch_paths_agree(B, auto):
         assert rmse(outs[sv][..., 0], outs[3][..., 0]) <= 1e-12, sv
 
 
+@pytest.mark.parametrize("N,B", ((1, 3), (2, 5), (63, 7), (65, 7), (129, 1100), (257, 5),
+                                 (512, 3)))
+def test_strict_scan_kernel_chunk_widths(N, B):
+    """The parallel-in-time kernel at the edges of its chunk widths (C = ⌈N/64⌉ = 1..8 slots
+    per lane; N = 65/129 leave the last lane one slot, N = 1 a single lane) and with 32 lanes per
+    instance (B = 1100 walks: 2200 instances beyond the resident waves) against the LQ kernel on
+    the same kicked walks: CoM within 1e-9, same statuses; and one window-mode step."""
+    zmax, zmin, x0, F, dt = synthetic_batch(B, 64 if N < 150 else 150, seed=N)
+    n = zmax.shape[1]
+    kick = dt * F / M
+    outs = []
+    for sv in (4, 3):
+        p = plan(N, strict=True, dt=dt).set_option("strict_solver", sv)
+        h, st = p.rollout(zmax, zmin, x0, kick=kick, kick_step=n // 2)
+        outs.append((h.cpu().numpy(), st.cpu().numpy()))
+        xw = x0[:, 1, :]
+        idx = np.minimum(np.arange(N), n - 1)
+        o, sts = p.step(xw, zmax[:, idx, 1], zmin[:, idx, 1])
+        outs.append((o.cpu().numpy(), sts.cpu().numpy()))
+    (h4, s4), (o4, t4), (h3, s3), (o3, t3) = outs
+    assert np.array_equal(s4, s3) and int(np.abs(s4).max()) == 0
+    assert np.abs(h4[..., 0] - h3[..., 0]).max() <= 1e-9
+    assert np.array_equal(t4, t3)
+    assert np.abs(o4 - o3).max() <= 1e-9 * max(1.0, np.abs(o3).max())
+
+
 @pytest.mark.parametrize("N,n", ((512, 1431), (150, 1100), (150, 2500), (256, 1000),
                                  (200, 3000)))
 def test_fft_correlation_equals_direct(N, n):
