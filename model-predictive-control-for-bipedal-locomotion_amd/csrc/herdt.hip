@@ -403,6 +403,9 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
   double* ktab = reinterpret_cast<double*>(hsm + ((3 * N * 64 + 15) & ~15) + sizeof(PolyLds));
   // (ktab row k: K0, K1, K2, 1/Huu; the all-free P after row k is in ptab, global, per
   // workgroup: sweep 2 starts its full rows from it)
+  // cen [MM+1][64]: the ZMP centre of each support segment after the footstep solve (0: the
+  // current foot, j: footstep j) — one LDS read per row instead of a select over MM footsteps
+  double* cen = ktab + N * 4;
   {
     // both sides' half-spaces and facet segments, once per workgroup
     const int sd = lane >> 5, i = lane & 31;
@@ -484,7 +487,7 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
   unsigned long long n_wave_pass = 0, n_pass = 0, n_m = 0, n_m2 = 0;
   unsigned itmax = 0;  // most passes of one solve (counter [9])
   unsigned long long pr_b = 0, pr_f = 0, pr_w = 0, pr_t0 = (kProf && a.prof) ? clock64() : 0;
-  unsigned long long pr_kw = 0, pr_ns = 0, pr_own = 0;
+  unsigned long long pr_kw = 0, pr_ns = 0, pr_own = 0, pr_fs = 0;
   const int64_t nsteps = a.window_mode ? 1 : a.n - 1;
   const int64_t kstep = (!a.window_mode && axis == 1 && a.kick) ? a.kick_step : -1;
   const double kv = (kstep >= 0 && valid) ? a.kick[wc] : 0.0;
@@ -498,18 +501,30 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
       return a.st[wc * a.ss + t];
     };
     int s_prev = cur, nbreak = 0, nstand = 0, lastbreak = -1;
-    for (int k = 0; k < N; ++k) {
-      const int sk = wstate(k);
-      segb[k * 64 + lane] = (unsigned char)nbreak;
-      const bool cont = (sk == s_prev) || (s_prev == ZMPC_DOUBLE_SUPPORT &&
-                                            sk == ZMPC_SINGLE_SUPPORT);
-      if (!cont) {
-        ++nbreak;
-        lastbreak = k;
+    // the window's states are loaded WB rows at a time, all in flight together (one row per
+    // round trip, at one wave per SIMD)
+    constexpr int WB = 16;
+    for (int k0 = 0; k0 < N; k0 += WB) {
+      int sv[WB];
+#pragma unroll
+      for (int r = 0; r < WB; ++r) sv[r] = wstate(min(k0 + r, N - 1));
+#pragma unroll
+      for (int r = 0; r < WB; ++r) {
+        const int k = k0 + r;
+        if (k < N) {
+          const int sk = sv[r];
+          segb[k * 64 + lane] = (unsigned char)nbreak;
+          const bool cont = (sk == s_prev) || (s_prev == ZMPC_DOUBLE_SUPPORT &&
+                                                sk == ZMPC_SINGLE_SUPPORT);
+          if (!cont) {
+            ++nbreak;
+            lastbreak = k;
+          }
+          s_prev = sk;
+          nstand += (sk == ZMPC_STANDING);
+          kind[k * 64 + lane] = (sk == ZMPC_STANDING) ? CK_STAND : CK_FOOT;
+        }
       }
-      s_prev = sk;
-      nstand += (sk == ZMPC_STANDING);
-      kind[k * 64 + lane] = (sk == ZMPC_STANDING) ? CK_STAND : CK_FOOT;
     }
     const int m = nbreak;                                // footsteps in the horizon
     int mw = valid ? m : 0;  // the wave's largest m (wave-uniform): sweep 1's column count
@@ -562,7 +577,7 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
       // Run at the wave's footstep count (NW = 3 + mw columns, wave-uniform): lanes with fewer
       // footsteps carry zero columns, and no lane pays for the MM − mw columns nobody has.
       double fx0 = 0.0;
-      unsigned long long tp1 = 0;
+      unsigned long long tp1 = 0, tpf = 0;
       int klane = -1;  // this lane's last pinned row (sweep 1 meets it first)
       auto sweep1 = [&](auto na_tag) {
         constexpr int NW = decltype(na_tag)::value;  // 3 + footstep columns
@@ -637,6 +652,7 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
             if (q < M) fsol[q] = fma(mu, e0[q], gf[q]);
         }
         if (m > 0) fsol[0] = fx0;  // (M = 0: the only footstep lies past the horizon)
+        if (kProf && a.prof) tpf = clock64();
       };
       switch (mw) {
         case 0: sweep1(std::integral_constant<int, 3>{}); break;
@@ -657,56 +673,62 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
       f0 = fx0;
       // ---- sweep 2: the 3-state Riccati with every ZMP centre known (c_k = fc or f_jf), whose
       // control law is the augmented one at f = fsol; slab rows: 4 doubles ---------------------
+      cen[lane] = fc;
+#pragma unroll
+      for (int q = 0; q < MM; ++q) cen[(q + 1) * 64 + lane] = fsol[q];
+      // (a segment past MM cannot occur: such a window flags ZMPC_ST_FACTOR above)
+      auto centre = [&](int sg) -> double { return cen[(sg <= MM ? sg : 0) * 64 + lane]; };
       {
         double P3[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0}, s3[3] = {0.0, 0.0, 0.0};
-        double vr_nx = vref(N - 1);
-        int sg_nx = segb[(N - 1) * 64 + lane], kd_nx = kind[(N - 1) * 64 + lane],
-            wk_nx = wset[(N - 1) * 64 + lane];
-        // free tail (rows past the wave's last pinned row): the s recursion with ktab's K, 1/Huu
-        for (int k = N - 1; k > kw; --k) {
-          const int sg = sg_nx;
-          const double vr = vr_nx;
-          {
-            const int k1 = k > 0 ? k - 1 : 0;
-            vr_nx = vref(k1);
-            sg_nx = segb[k1 * 64 + lane];
-            kd_nx = kind[k1 * 64 + lane];
-            wk_nx = wset[k1 * 64 + lane];
-          }
-          double ck = fc;
-#pragma unroll
-          for (int q = 0; q < MM; ++q)
-            if (sg - 1 == q) ck = fsol[q];
-          double kff;
-          herdt_tail_row(rc, s3, vr, ck, ktab + k * 4, kff);
-          S(k, 3) = kff;
-        }
         if (kw >= 0 && kw + 1 < N) {
 #pragma unroll
           for (int q = 0; q < 6; ++q) P3[q] = ptab[(kw + 1) * 6 + q];  // V_{kw+1}, all free
         }
-        for (int k = kw; k >= 0; --k) {
-          const int sg = sg_nx, kd = kd_nx, wk = wk_nx;
-          const double vr = vr_nx;
-          {
-            const int k1 = k > 0 ? k - 1 : 0;
-            vr_nx = vref(k1);
-            sg_nx = segb[k1 * 64 + lane];
-            kd_nx = kind[k1 * 64 + lane];
-            wk_nx = wset[k1 * 64 + lane];
-          }
-          double ck = fc;
+        // v_ref rows arrive in blocks of VB, each block's loads issued one block ahead and
+        // before the slab stores of the block in hand (vector loads and stores retire through
+        // one in-order counter, vmcnt: a load issued after a row's stores is waited for only
+        // once those stores are acknowledged)
+        constexpr int VB = 8;
+        double vb[VB], vn[VB];
 #pragma unroll
-          for (int q = 0; q < MM; ++q)
-            if (sg - 1 == q) ck = fsol[q];
-          double pbx[3], sb, Kx[3], kff;
-          herdt_row<3>(rc, P3, s3, vr, ck, -1, kd, wk, pbx, sb, Kx, kff);
-          // slab row: the control law of a free row, the costate map of a pinned one
-          const bool pin = wk != 0;
-          S(k, 0) = pin ? pbx[0] : Kx[0];
-          S(k, 1) = pin ? pbx[1] : Kx[1];
-          S(k, 2) = pin ? pbx[2] : Kx[2];
-          S(k, 3) = pin ? sb : kff;
+        for (int r = 0; r < VB; ++r) vb[r] = vref(max(N - 1 - r, 0));
+        for (int k0 = N - 1; k0 >= 0; k0 -= VB) {
+#pragma unroll
+          for (int r = 0; r < VB; ++r) vn[r] = vref(max(k0 - VB - r, 0));
+          int sgb[VB], kdb[VB], wkb[VB];  // the block's LDS row bytes, all in flight together
+#pragma unroll
+          for (int r = 0; r < VB; ++r) {
+            const int k = max(k0 - r, 0);
+            sgb[r] = segb[k * 64 + lane];
+            kdb[r] = kind[k * 64 + lane];
+            wkb[r] = wset[k * 64 + lane];
+          }
+#pragma unroll
+          for (int r = 0; r < VB; ++r) {
+            const int k = k0 - r;
+            if (k >= 0) {
+              const double ck = centre(sgb[r]);
+              if (k > kw) {
+                // free tail (rows past the wave's last pinned row): the s recursion with
+                // ktab's K, 1/Huu
+                double kff;
+                herdt_tail_row(rc, s3, vb[r], ck, ktab + k * 4, kff);
+                S(k, 3) = kff;
+              } else {
+                const int kd = kdb[r], wk = wkb[r];
+                double pbx[3], sb, Kx[3], kff;
+                herdt_row<3>(rc, P3, s3, vb[r], ck, -1, kd, wk, pbx, sb, Kx, kff);
+                // slab row: the control law of a free row, the costate map of a pinned one
+                const bool pin = wk != 0;
+                S(k, 0) = pin ? pbx[0] : Kx[0];
+                S(k, 1) = pin ? pbx[1] : Kx[1];
+                S(k, 2) = pin ? pbx[2] : Kx[2];
+                S(k, 3) = pin ? sb : kff;
+              }
+            }
+          }
+#pragma unroll
+          for (int r = 0; r < VB; ++r) vb[r] = vn[r];
         }
       }
       // ---- forward: roll out, primal check of the free rows, dual check of the pinned rows --
@@ -751,11 +773,8 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
             for (int r = 0; r < RB; ++r) {
               const int k = k0 + r;
               if (k < ke) {
-                const int sg = sgb[r], kd = kdb[r], wk = wkb[r];
-                double ccost = fc;
-#pragma unroll
-                for (int q = 0; q < MM; ++q)
-                  if (sg - 1 == q) ccost = fsol[q];
+                const int kd = kdb[r], wk = wkb[r];
+                const double ccost = centre(sgb[r]);
                 double u;
                 if (wk == 0) {
                   u = -(fk[r][0] * xs[0] + fk[r][1] * xs[1] + fk[r][2] * xs[2]) - fk[r][3];
@@ -817,6 +836,7 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
         const unsigned long long tp3 = clock64();
         pr_b += tp1 - tp0;
         pr_f += tp2 - tp1;
+        pr_fs += tpf - tp1;
         pr_w += tp3 - tp2;
       }
       ++it;
@@ -915,6 +935,7 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
       atomicAdd(a.prof + 5, pr_ns);
       atomicAdd(a.prof + 6, n_wave_pass);
       atomicAdd(a.prof + 7, pr_own);
+      atomicAdd(a.prof + 8, pr_fs);
     }
   }
   if (a.cnt) {
@@ -985,11 +1006,11 @@ hipError_t zmpc_launch_herdt(const zmpc_plan* p, const zmpc_herdt_params* prm, i
 #ifdef ZMPC_DIAG
   static unsigned long long* prof = [] {  // diagnostics build: per-phase clocks to stderr
     unsigned long long* q = nullptr;
-    if (getenv("ZMPC_HERDT_PROF") && hipMalloc((void**)&q, 8 * sizeof(unsigned long long)) != hipSuccess)
+    if (getenv("ZMPC_HERDT_PROF") && hipMalloc((void**)&q, 9 * sizeof(unsigned long long)) != hipSuccess)
       q = nullptr;
     return q;
   }();
-  if (prof) (void)hipMemsetAsync(prof, 0, 8 * sizeof(unsigned long long), s);
+  if (prof) (void)hipMemsetAsync(prof, 0, 9 * sizeof(unsigned long long), s);
   a.prof = prof;
 #else
   a.prof = nullptr;
@@ -1009,7 +1030,7 @@ hipError_t zmpc_launch_herdt(const zmpc_plan* p, const zmpc_herdt_params* prm, i
     return hipErrorOutOfMemory;
   }
   const size_t lds = (((size_t)3 * a.N * 64 + 15) & ~(size_t)15) + sizeof(PolyLds) +
-                     (size_t)a.N * 4 * sizeof(double);
+                     (size_t)a.N * 4 * sizeof(double) + (size_t)(8 + 1) * 64 * sizeof(double);
   if (lds > 160 * 1024) {
     (void)hipFreeAsync(a.ws, s);
     *why = "horizon too long for the Herdt solver's LDS flags";
@@ -1035,15 +1056,16 @@ hipError_t zmpc_launch_herdt(const zmpc_plan* p, const zmpc_herdt_params* prm, i
   hipError_t e = hipGetLastError();
   const hipError_t ef = hipFreeAsync(a.ws, s);
   if (a.prof && e == hipSuccess) {
-    unsigned long long h[8];
+    unsigned long long h[9];
     (void)hipMemcpy(h, a.prof, sizeof(h), hipMemcpyDeviceToHost);
     const double t = (double)(h[3] ? h[3] : 1), wp = (double)(h[6] ? h[6] : 1);
     fprintf(stderr,
-            "herdt prof: backward %.3f footsteps %.3f forward %.3f (of %llu clocks/wave); "
+            "herdt prof: backward %.3f footsteps+sweep2 %.3f (footsteps alone %.3f) forward %.3f "
+            "(of %llu clocks/wave); "
             "rows to the wave's last pinned row %.1f, pinned rows per lane %.2f (per pass); "
             "lane-pair passes needed %llu vs wave passes x 64 %llu\n",
-            h[0] / t, h[1] / t, h[2] / t, h[3] / (unsigned long long)blocks, h[4] / wp,
-            h[5] / (wp * 64), h[7], h[6] * 64);
+            h[0] / t, h[1] / t, h[8] / t, h[2] / t, h[3] / (unsigned long long)blocks,
+            h[4] / wp, h[5] / (wp * 64), h[7], h[6] * 64);
   }
   return e != hipSuccess ? e : ef;
 }

@@ -1,0 +1,28 @@
+#!/bin/bash
+# Round 4 GPU session s: Herdt light sweep 2 + shared v_ref staged in LDS + packed row bytes —
+# tests, output check vs the last commit's build, config 6 alternated (this build, the
+# centres-only build, the light build without LDS v_ref), per-phase clocks with the footstep
+# solve timed apart (diagnostics builds).
+set -u
+OUT=gpurun_out/${1:-r4s}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+step() { echo "== $1 rc=$2"; if [ "$2" -ne 0 ]; then exit "$2"; fi; }
+L=model-predictive-control-for-bipedal-locomotion_amd/mpc_bipedal
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider \
+  -k herdt > "$OUT/pytest.log" 2>&1
+step pytest $?; tail -1 "$OUT/pytest.log"
+ZMPC_LIB=$PWD/$L/libzmpc.so timeout -k 10 120 python scripts/herdt_once.py 512 /tmp/new.npy > "$OUT/once_new.log" 2>&1
+step once_new $?
+ZMPC_LIB=$PWD/$L/ab/libzmpc_hbase.so timeout -k 10 120 python scripts/herdt_once.py 512 /tmp/old.npy > "$OUT/once_old.log" 2>&1
+step once_old $?
+python3 -c "import numpy as np; a=np.load('/tmp/new.npy'); b=np.load('/tmp/old.npy'); print('bitwise equal', np.array_equal(a,b,equal_nan=True), 'max abs diff', np.nanmax(np.abs(a-b)), 'nan pattern equal', np.array_equal(np.isnan(a), np.isnan(b)))"
+for v in base hcen light2 base hcen light2; do
+  if [ $v = base ]; then lib=$PWD/$L/libzmpc.so; else lib=$PWD/$L/ab/libzmpc_$v.so; fi
+  ZMPC_LIB=$lib timeout -k 10 300 python bench.py --config 6 --steps 5 --warmup 2 --no-cpu-baseline > "$OUT/bench_c6_$v.json" 2> "$OUT/bench_c6_$v.err"
+  step "config6 $v" $?; python3 -c "import json; d=json.loads(open('$OUT/bench_c6_$v.json').read().strip().splitlines()[-1]); print('$v', d['ms_per_step'], d['roofline'].get('kernel_ms'), d['roofline'].get('passes_per_solve'), d.get('com_rmse_vs_ref'))"
+done
+for v in hbase_diag light3_diag; do
+  ZMPC_HERDT_PROF=1 ZMPC_LIB=$PWD/$L/ab/libzmpc_$v.so timeout -k 10 180 python scripts/herdt_once.py 32768 > "$OUT/prof_$v.log" 2>&1
+  step "prof $v" $?; grep "herdt prof" "$OUT/prof_$v.log" | tail -1
+done

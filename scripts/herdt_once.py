@@ -1,5 +1,5 @@
 """One batched Herdt rollout (config 6 inputs) after a warm-up, for rocprofv3 counter passes:
-python scripts/herdt_once.py [B]"""
+python scripts/herdt_once.py [B] [out.npy]  (out.npy: the history, for bitwise A/B of builds)"""
 import os
 import sys
 
@@ -33,3 +33,5 @@ for _ in range(2):
     hist, foot, status = plan.herdt_rollout(prm, v, s_t, nb_t, x0, kick=kick, kick_step=n // 2)
 torch.cuda.synchronize()
 print("status max", int(status.abs().max()), plan.counters())
+if len(sys.argv) > 2:
+    np.save(sys.argv[2], torch.cat([hist.reshape(B, -1), foot.reshape(B, -1)], 1).cpu().numpy())
