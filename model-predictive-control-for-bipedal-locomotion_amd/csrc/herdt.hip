@@ -291,7 +291,19 @@ __device__ __forceinline__ void herdt_row(const RowC& c, double* P, double* s, d
   for (int q = 3; q < NA; ++q) hx[q] = s[q];
   // control law u = −K̂ ξ − kff
   double Kh[NA], kff;
-  if (wk == 0) {
+  if constexpr (NA == 3) {
+    // the 3-state row (sweep 2): both laws, merged by selects (no divergent branch)
+    double iq = __builtin_amdgcn_rcp(Huu);
+    iq = fma(iq, fma(-Huu, iq, 1.0), iq);
+    iq = fma(iq, fma(-Huu, iq, 1.0), iq);
+    const bool pin = wk != 0;
+    const double t = (kd == CK_STAND) ? (wk == 1 ? c.shi : c.slo) : (wk == 1 ? c.bnd : -c.bnd);
+    const double cc0 = (kd == CK_FOOT) ? fc0 : 0.0;
+    const double ip = c.ip;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) Kh[q] = pin ? c1[q] * ip : Hu[q] * iq;
+    kff = pin ? -(t + cc0) * ip : -hu * iq;
+  } else if (wk == 0) {
     // 1/Huu: hardware reciprocal + two Newton steps (Huu ≥ α + βb_v² + γp0² > 0)
     double iq = __builtin_amdgcn_rcp(Huu);
     iq = fma(iq, fma(-Huu, iq, 1.0), iq);
@@ -487,7 +499,7 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
   unsigned long long n_wave_pass = 0, n_pass = 0, n_m = 0, n_m2 = 0;
   unsigned itmax = 0;  // most passes of one solve (counter [9])
   unsigned long long pr_b = 0, pr_f = 0, pr_w = 0, pr_t0 = (kProf && a.prof) ? clock64() : 0;
-  unsigned long long pr_kw = 0, pr_ns = 0, pr_own = 0, pr_fs = 0;
+  unsigned long long pr_kw = 0, pr_ns = 0, pr_own = 0, pr_fs = 0, pr_lw = 0;
   const int64_t nsteps = a.window_mode ? 1 : a.n - 1;
   const int64_t kstep = (!a.window_mode && axis == 1 && a.kick) ? a.kick_step : -1;
   const double kv = (kstep >= 0 && valid) ? a.kick[wc] : 0.0;
@@ -769,24 +781,32 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
               kdb[r] = kind[k * 64 + lane];
               wkb[r] = TAIL ? 0 : wset[k * 64 + lane];
             }
+            if (kProf && a.prof) {
+              // diagnostics: how long the block's loads keep the wave waiting
+              const unsigned long long tw = clock64();
+              __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) (gfx9 encoding)
+              pr_lw += clock64() - tw;
+            }
 #pragma unroll
             for (int r = 0; r < RB; ++r) {
               const int k = k0 + r;
               if (k < ke) {
+                // branch-free: both control laws and both checks, merged by selects (at one
+                // wave per SIMD the exec-mask bookkeeping of divergent free/pinned rows cost
+                // more than the arithmetic it skipped)
                 const int kd = kdb[r], wk = wkb[r];
                 const double ccost = centre(sgb[r]);
-                double u;
-                if (wk == 0) {
-                  u = -(fk[r][0] * xs[0] + fk[r][1] * xs[1] + fk[r][2] * xs[2]) - fk[r][3];
-                } else {
-                  // pinned: c1ᵀx + p0 u − ccon = t (ccon: the ZMP centre on a foot row)
-                  const double t =
-                      (kd == CK_STAND) ? (wk == 1 ? shi : slo) : (wk == 1 ? bnd : -bnd);
-                  const double ccon = (kd == CK_FOOT) ? ccost : 0.0;
-                  u = (t + ccon - (c1[0] * xs[0] + c1[1] * xs[1] + c1[2] * xs[2])) * ip0;
-                }
+                const bool pin = wk != 0, foot = kd == CK_FOOT;
+                const double hi = foot ? bnd : shi, lo = foot ? -bnd : slo;
+                const double ccon = foot ? ccost : 0.0;
+                const double cx = c1[0] * xs[0] + c1[1] * xs[1] + c1[2] * xs[2];
+                // free: u = −K x − kff; pinned: c1ᵀx + p0 u − ccon = t (ccon: the foot centre)
+                const double ufree =
+                    -(fk[r][0] * xs[0] + fk[r][1] * xs[1] + fk[r][2] * xs[2]) - fk[r][3];
+                const double upin = ((wk == 1 ? hi : lo) + ccon - cx) * ip0;
+                const double u = pin ? upin : ufree;
                 if (k == 0) u0 = u;
-                const double z = c1[0] * xs[0] + c1[1] * xs[1] + c1[2] * xs[2] + p0 * u;
+                const double z = cx + p0 * u;
                 const double v = ev[1] * xs[1] + ev[2] * xs[2] + bv * u;
                 const double y0 = xs[0] + T * xs[1] + T2 * xs[2] + T3 * u;
                 const double y1 = xs[1] + T * xs[2] + T2 * u;
@@ -794,28 +814,20 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
                 xs[0] = y0;
                 xs[1] = y1;
                 xs[2] = y2;
-                if (wk == 0) {
-                  if (kd != CK_NONE) {
-                    const double tol = 1e-11;
-                    const double zz = (kd == CK_FOOT) ? z - ccost : z;
-                    const double hi = (kd == CK_FOOT) ? bnd : shi,
-                                 lo = (kd == CK_FOOT) ? -bnd : slo;
-                    const int nf = (zz > hi + tol) ? 1 : ((zz < lo - tol) ? 2 : 0);
-                    if (nf) {
-                      wset[k * 64 + lane] = (unsigned char)nf;
-                      changed = true;
-                    }
-                  }
-                } else {
-                  const double bl = fk[r][0] * y0 + fk[r][1] * y1 + fk[r][2] * y2 - fk[r][3];
-                  const double gu =
-                      al * u + be * bv * (v - vrb[r]) + ga * p0 * (z - ccost) + bl;
-                  const double nu = -gu * ip0;  // ≥ 0 at an upper, ≤ 0 at a lower bound
-                  const double tn = 1e-10 * (1.0 + fabs(nu));
-                  if ((wk == 1 && nu < -tn) || (wk == 2 && nu > tn)) {
-                    wset[k * 64 + lane] = 0;
-                    changed = true;
-                  }
+                // primal check of a free row with a constraint
+                const double tol = 1e-11;
+                const double zz = z - ccon;
+                const int nf = (zz > hi + tol) ? 1 : ((zz < lo - tol) ? 2 : 0);
+                // a pinned row's multiplier (slab: (PB̂)_x, B̂ᵀs of V_{k+1})
+                const double bl = fk[r][0] * y0 + fk[r][1] * y1 + fk[r][2] * y2 - fk[r][3];
+                const double gu = al * u + be * bv * (v - vrb[r]) + ga * p0 * (z - ccost) + bl;
+                const double nu = -gu * ip0;  // ≥ 0 at an upper, ≤ 0 at a lower bound
+                const double tn = 1e-10 * (1.0 + fabs(nu));
+                const bool drop = (wk == 1 && nu < -tn) || (wk == 2 && nu > tn);
+                const int nw = pin ? (drop ? 0 : wk) : (kd != CK_NONE ? nf : 0);
+                if (nw != wk) {
+                  wset[k * 64 + lane] = (unsigned char)nw;
+                  changed = true;
                 }
               }
             }
@@ -936,6 +948,7 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
       atomicAdd(a.prof + 6, n_wave_pass);
       atomicAdd(a.prof + 7, pr_own);
       atomicAdd(a.prof + 8, pr_fs);
+      atomicAdd(a.prof + 9, pr_lw);
     }
   }
   if (a.cnt) {
@@ -1006,11 +1019,11 @@ hipError_t zmpc_launch_herdt(const zmpc_plan* p, const zmpc_herdt_params* prm, i
 #ifdef ZMPC_DIAG
   static unsigned long long* prof = [] {  // diagnostics build: per-phase clocks to stderr
     unsigned long long* q = nullptr;
-    if (getenv("ZMPC_HERDT_PROF") && hipMalloc((void**)&q, 9 * sizeof(unsigned long long)) != hipSuccess)
+    if (getenv("ZMPC_HERDT_PROF") && hipMalloc((void**)&q, 10 * sizeof(unsigned long long)) != hipSuccess)
       q = nullptr;
     return q;
   }();
-  if (prof) (void)hipMemsetAsync(prof, 0, 9 * sizeof(unsigned long long), s);
+  if (prof) (void)hipMemsetAsync(prof, 0, 10 * sizeof(unsigned long long), s);
   a.prof = prof;
 #else
   a.prof = nullptr;
@@ -1056,15 +1069,15 @@ hipError_t zmpc_launch_herdt(const zmpc_plan* p, const zmpc_herdt_params* prm, i
   hipError_t e = hipGetLastError();
   const hipError_t ef = hipFreeAsync(a.ws, s);
   if (a.prof && e == hipSuccess) {
-    unsigned long long h[9];
+    unsigned long long h[10];
     (void)hipMemcpy(h, a.prof, sizeof(h), hipMemcpyDeviceToHost);
     const double t = (double)(h[3] ? h[3] : 1), wp = (double)(h[6] ? h[6] : 1);
     fprintf(stderr,
             "herdt prof: backward %.3f footsteps+sweep2 %.3f (footsteps alone %.3f) forward %.3f "
-            "(of %llu clocks/wave); "
+            "(its slab-load waits %.3f) (of %llu clocks/wave); "
             "rows to the wave's last pinned row %.1f, pinned rows per lane %.2f (per pass); "
             "lane-pair passes needed %llu vs wave passes x 64 %llu\n",
-            h[0] / t, h[1] / t, h[8] / t, h[2] / t, h[3] / (unsigned long long)blocks,
+            h[0] / t, h[1] / t, h[8] / t, h[2] / t, h[9] / t, h[3] / (unsigned long long)blocks,
             h[4] / wp, h[5] / (wp * 64), h[7], h[6] * 64);
   }
   return e != hipSuccess ? e : ef;
