@@ -291,38 +291,23 @@ __device__ __forceinline__ void herdt_row(const RowC& c, double* P, double* s, d
   for (int q = 3; q < NA; ++q) hx[q] = s[q];
   // control law u = −K̂ ξ − kff
   double Kh[NA], kff;
-  if constexpr (NA == 3) {
-    // the 3-state row (sweep 2): both laws, merged by selects (no divergent branch)
+  {
+    // both laws, merged by selects: a wave with free and pinned lanes would otherwise run both
+    // sides of a branch with its exec-mask bookkeeping, at one wave per SIMD
+    // free: 1/Huu by the hardware reciprocal + two Newton steps (Huu ≥ α + βb_v² + γp0² > 0)
     double iq = __builtin_amdgcn_rcp(Huu);
     iq = fma(iq, fma(-Huu, iq, 1.0), iq);
     iq = fma(iq, fma(-Huu, iq, 1.0), iq);
-    const bool pin = wk != 0;
-    const double t = (kd == CK_STAND) ? (wk == 1 ? c.shi : c.slo) : (wk == 1 ? c.bnd : -c.bnd);
-    const double cc0 = (kd == CK_FOOT) ? fc0 : 0.0;
-    const double ip = c.ip;
-#pragma unroll
-    for (int q = 0; q < 3; ++q) Kh[q] = pin ? c1[q] * ip : Hu[q] * iq;
-    kff = pin ? -(t + cc0) * ip : -hu * iq;
-  } else if (wk == 0) {
-    // 1/Huu: hardware reciprocal + two Newton steps (Huu ≥ α + βb_v² + γp0² > 0)
-    double iq = __builtin_amdgcn_rcp(Huu);
-    iq = fma(iq, fma(-Huu, iq, 1.0), iq);
-    iq = fma(iq, fma(-Huu, iq, 1.0), iq);
-#pragma unroll
-    for (int q = 0; q < NA; ++q) Kh[q] = Hu[q] * iq;
-    kff = -hu * iq;
-  } else {
     // pinned: c1ᵀx + p0 u − ccon = t  (ccon: the foot centre on a foot row, 0 standing)
-    const bool foot = kd == CK_FOOT;
+    const bool pin = wk != 0, foot = kd == CK_FOOT;
     const double t = (kd == CK_STAND) ? (wk == 1 ? c.shi : c.slo) : (wk == 1 ? c.bnd : -c.bnd);
     const double cc0 = foot ? fc0 : 0.0;
     const double ip = c.ip;
-    Kh[0] = c1[0] * ip;
-    Kh[1] = c1[1] * ip;
-    Kh[2] = c1[2] * ip;
 #pragma unroll
-    for (int q = 3; q < NA; ++q) Kh[q] = (foot && q - 3 == jf) ? -ip : 0.0;
-    kff = -(t + cc0) * ip;
+    for (int q = 0; q < 3; ++q) Kh[q] = pin ? c1[q] * ip : Hu[q] * iq;
+#pragma unroll
+    for (int q = 3; q < NA; ++q) Kh[q] = pin ? ((foot && q - 3 == jf) ? -ip : 0.0) : Hu[q] * iq;
+    kff = pin ? -(t + cc0) * ip : -hu * iq;
   }
   // D = Huu·K̂ − Hu (the pinned rows' correction; a free row's rounding residue), formed where
   // it is used so that only Hu and K̂ stay live through the update
