@@ -211,6 +211,16 @@ __device__ __forceinline__ RunCursor run_bwd(const Lane& L, int ci) {
 template <int S, bool FWD>
 __device__ __forceinline__ void seg_runs(const Lane& L, int t0, RunCursor& c, double* r,
                                          double* h) {
+  // most segments lie inside one run for every lane: one test per segment, and the per-slot
+  // crossing branches (with their exec-mask bookkeeping) only where a lane crosses
+  if (FWD ? (t0 + S - 1 < c.e1) : (t0 >= c.e1)) {
+#pragma unroll
+    for (int q = 0; q < S; ++q) {
+      r[q] = c.r;
+      h[q] = c.h;
+    }
+    return;
+  }
   if constexpr (FWD) {
 #pragma unroll
     for (int q = 0; q < S; ++q) {
