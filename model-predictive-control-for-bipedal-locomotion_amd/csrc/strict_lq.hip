@@ -106,6 +106,13 @@ struct LqArgs {
   double pig;            // π γ'
   double rho, quu0;      // ρ, π² + ρ
   double tolnu;          // multiplier tolerance in the scaled objective (1e-13 / Q)
+  // task queue (rollouts with more waves than the chip holds): the grid is the resident
+  // blocks; each wave runs its own task first (gw), then takes the next from *queue:
+  // queue index q → the remaining blocks' y waves first (the heavier axis), then their x
+  // waves.  null: one task per wave (gw).
+  int* queue;
+  int64_t qblock0;       // first block not in the grid
+  int64_t nblocks;       // blocks of the whole launch (G waves each)
 };
 
 template <int S>
@@ -525,7 +532,11 @@ __device__ __forceinline__ void ck_load_s(const CkIO<NT>& io, const double* ck, 
 // waves of 32 walks × both axes, so that every SIMD keeps two y-carrying waves to the end, are
 // slower — config 3 87.0 vs 64.9 ms: the x lanes then run the working-set form up to the wave's
 // last pinned slot, 0.76 of the pass-slots instead of 0.48, profiles/r4/r4l_*.)
-template <int S, int G, bool NT, bool RUNS>
+// QUEUE: a grid of the resident blocks whose waves loop over tasks (a.queue); without it each
+// wave runs its one task and the loop folds away (the task loop's live ranges cost the Riccati
+// sweeps ≈75 more spilled registers: config 3 61.4 → 65.7 ms, so only launches with more
+// blocks than the chip holds take the queue form, profiles/r4/r4z/).
+template <int S, int G, bool NT, bool RUNS, bool QUEUE>
 __global__ void __launch_bounds__(64 * G, 2)
     zmpc_strict_lq_kernel(LqArgs a, const double* __restrict__ tab) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lq_smem[];
@@ -537,17 +548,27 @@ __global__ void __launch_bounds__(64 * G, 2)
   const Flags fl{reinterpret_cast<signed char*>(lq_smem) + (size_t)wave * fbytes * 64};
   double* ck = a.ck + (size_t)gw * a.NS * kCkStride;
   const CkIO<NT> io{};
+  unsigned long long n_wave_pass = 0, n_lane_pass = 0, n_ws_slots = 0;
+#ifdef ZMPC_DIAG
+  unsigned long long n_sb_ws = 0, n_sb_free = 0;
+#endif
+  unsigned itmax = 0;  // most passes of one of this lane's solves (counter [8])
+  int64_t task = gw;   // this wave's (group, axis): gw's own first, then from the queue
+  for (;;) {
+  // (the task's block and wave: the kernel's own without a queue)
+  const int64_t tblk = QUEUE ? task / G : (int64_t)blockIdx.x;
+  const int twave = QUEUE ? (int)(task % G) : wave;
   int axis;
   int64_t pos;  // the lane's walk position (order.hip's kick order, or the walk itself)
   if (a.window_mode) {
     axis = 0;
-    pos = gw * 64 + lane;
+    pos = task * 64 + lane;
   } else if (G == 8) {
-    axis = wave >> 2;
-    pos = ((int64_t)blockIdx.x * 4 + (wave & 3)) * 64 + lane;
+    axis = twave >> 2;
+    pos = (tblk * 4 + (twave & 3)) * 64 + lane;
   } else {
-    axis = (int)(gw & 1);
-    pos = (gw >> 1) * 64 + lane;
+    axis = (int)(task & 1);
+    pos = (task >> 1) * 64 + lane;
   }
   // lane position pos runs walk b (the kick order of order.hip, or the identity); the staged
   // bounds follow the positions (table (axis, pos / 64), column pos % 64), everything per walk
@@ -592,10 +613,6 @@ __global__ void __launch_bounds__(64 * G, 2)
     }
   }
   int fq = 0;
-  unsigned long long n_wave_pass = 0, n_lane_pass = 0, n_ws_slots = 0;
-#ifdef ZMPC_DIAG
-  unsigned long long n_sb_ws = 0, n_sb_free = 0;
-#endif
   const int64_t kstep =
       (!a.window_mode && axis == 1 && a.kick != nullptr && valid)
           ? (a.kick_steps ? a.kick_steps[b] : a.kick_step)
@@ -609,7 +626,6 @@ __global__ void __launch_bounds__(64 * G, 2)
   int64_t i = 0;
   bool active = valid && a.nsteps > 0;
   int it = 0;
-  unsigned itmax = 0;  // most passes of one of this lane's solves (counter [8])
   int klast = -1;      // last pinned slot of this lane's working set (−1: none)
   while (__any(active)) {
     ++n_wave_pass;
@@ -777,6 +793,21 @@ __global__ void __launch_bounds__(64 * G, 2)
     else if (fq != 0)
       atomicOr(&a.status[b], fq);
   }
+  if constexpr (QUEUE && G == 8) {
+    // the next task: one device-scope atomic per task (a task is a whole rollout of 64 walks)
+    int q = 0;
+    if (lane == 0) q = atomicAdd(a.queue, 1);
+    q = __builtin_amdgcn_readfirstlane(__shfl(q, 0, 64));
+    const int64_t rem = a.nblocks - a.qblock0;      // blocks not in the grid
+    const int64_t half = rem * (G / 2);              // their y waves (G = 8: waves 4..7)
+    if (q >= 2 * half) break;
+    const int64_t qq = q < half ? q : q - half;
+    const int64_t blk = a.qblock0 + qq / (G / 2);
+    task = blk * G + (q < half ? G / 2 : 0) + qq % (G / 2);
+  } else {
+    break;  // one task per wave (the host takes the queue form for 8-wave blocks only)
+  }
+  }
   if (a.cnt) {
     for (int o = 32; o > 0; o >>= 1) {
       n_lane_pass += __shfl_xor(n_lane_pass, o);
@@ -930,18 +961,25 @@ struct LqVariant {
   void (*kernel_nt)(LqArgs, const double*);  // checkpoints non-temporal (per-walk bounds)
   void (*kernel_runs)(LqArgs, const double*);     // run-length bounds, cached checkpoints
   void (*kernel_runs_nt)(LqArgs, const double*);  // run-length bounds, non-temporal
+  // the same four with the task queue (G = 8 only; null otherwise)
+  void (*q_kernel)(LqArgs, const double*);
+  void (*q_kernel_nt)(LqArgs, const double*);
+  void (*q_kernel_runs)(LqArgs, const double*);
+  void (*q_kernel_runs_nt)(LqArgs, const double*);
 };
 
-#define ZMPC_LQV(G)                                                                        \
-  {G, zmpc_strict_lq_kernel<LQ_S, G, false, false>, zmpc_strict_lq_kernel<LQ_S, G, true, false>, \
-   zmpc_strict_lq_kernel<LQ_S, G, false, true>, zmpc_strict_lq_kernel<LQ_S, G, true, true>}
+#define ZMPC_LQK(G, Q)                                                               \
+  zmpc_strict_lq_kernel<LQ_S, G, false, false, Q>, zmpc_strict_lq_kernel<LQ_S, G, true, false, Q>, \
+      zmpc_strict_lq_kernel<LQ_S, G, false, true, Q>, zmpc_strict_lq_kernel<LQ_S, G, true, true, Q>
+#define ZMPC_LQV(G) {G, ZMPC_LQK(G, false), nullptr, nullptr, nullptr, nullptr}
 const LqVariant kLqVariants[] = {
-    ZMPC_LQV(8),  // default
+    {8, ZMPC_LQK(8, false), ZMPC_LQK(8, true)},  // default
     ZMPC_LQV(4),  // N up to 640
     ZMPC_LQV(2),  // N up to 1280
     ZMPC_LQV(1),  // N up to 2560
 };
 #undef ZMPC_LQV
+#undef ZMPC_LQK
 constexpr size_t kLdsCap = 160 * 1024;
 
 // LDS of one workgroup: the G waves' slot flags.
@@ -986,7 +1024,33 @@ hipError_t launch_lq(const zmpc_plan* p, LqArgs& a, int64_t waves, hipStream_t s
   // rollouts over per-walk bounds: non-temporal checkpoints (see CkIO)
   const bool nt = !a.window_mode && !a.shared;
   auto k = a.rs ? (nt ? var->kernel_runs_nt : var->kernel_runs) : (nt ? var->kernel_nt : var->kernel);
-  hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(64 * var->G), lds, s, a,
+  auto kq = a.rs ? (nt ? var->q_kernel_runs_nt : var->q_kernel_runs)
+                 : (nt ? var->q_kernel_nt : var->q_kernel);
+  // more blocks than the chip holds at once: a grid of the resident blocks and a task queue
+  // (an x wave is done long before its SIMD's y wave; with one task per wave its slot idles
+  // until the whole block has finished, while a queue refills it with the next y wave)
+  int64_t grid = blocks;
+  int* queue = a.queue;
+  a.queue = nullptr;
+  if (queue != nullptr && kq != nullptr && !a.window_mode) {
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kq, 64 * var->G, lds) !=
+        hipSuccess) {
+      (void)hipGetLastError();
+      per_cu = 0;
+    }
+    const int64_t resident = (int64_t)per_cu * (p->cus > 0 ? p->cus : 0);
+    if (resident > 0 && blocks > resident) {
+      hipError_t e = hipMemsetAsync(queue, 0, sizeof(int), s);
+      if (e != hipSuccess) return e;
+      grid = resident;
+      k = kq;
+      a.queue = queue;
+      a.qblock0 = resident;
+      a.nblocks = blocks;
+    }
+  }
+  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(64 * var->G), lds, s, a,
                      (const double*)p->lqtab);
   return hipGetLastError();
 }
@@ -996,8 +1060,9 @@ hipError_t launch_lq(const zmpc_plan* p, LqArgs& a, int64_t waves, hipStream_t s
 hipError_t zmpc_strict_lq_set_attrs() {
   hipError_t e = hipSuccess;
   for (const LqVariant& c : kLqVariants)
-    for (auto k : {c.kernel, c.kernel_nt, c.kernel_runs, c.kernel_runs_nt})
-      if (e == hipSuccess)
+    for (auto k : {c.kernel, c.kernel_nt, c.kernel_runs, c.kernel_runs_nt, c.q_kernel,
+                   c.q_kernel_nt, c.q_kernel_runs, c.q_kernel_runs_nt})
+      if (k != nullptr && e == hipSuccess)
         e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 160 * 1024);
   return e;
@@ -1064,12 +1129,13 @@ hipError_t zmpc_launch_rollout_strict_lq(const zmpc_plan* p, int64_t B, int64_t 
   const size_t ord_doubles = ordered ? (zmpc_kick_order_bytes(B) + 7) / 8 : 0;
   double* ws = nullptr;
   if (hipMallocAsync((void**)&ws,
-                     (ck_doubles + st_doubles + perm_doubles + ord_doubles) * sizeof(double),
+                     (ck_doubles + st_doubles + perm_doubles + ord_doubles + 1) * sizeof(double),
                      s) != hipSuccess) {
     (void)hipGetLastError();
     return hipErrorOutOfMemory;  // ZMPC_ENOMEM at the C-ABI
   }
   a.ck = ws;
+  a.queue = reinterpret_cast<int*>(ws + ck_doubles + st_doubles + perm_doubles + ord_doubles);
   double2* hl = reinterpret_cast<double2*>(ws + ck_doubles);
   a.perm = nullptr;
   if (ordered) {
