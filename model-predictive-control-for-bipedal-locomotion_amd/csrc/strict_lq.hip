@@ -533,9 +533,10 @@ __device__ __forceinline__ void ck_load_s(const CkIO<NT>& io, const double* ck, 
 // slower — config 3 87.0 vs 64.9 ms: the x lanes then run the working-set form up to the wave's
 // last pinned slot, 0.76 of the pass-slots instead of 0.48, profiles/r4/r4l_*.)
 // QUEUE: a grid of the resident blocks whose waves loop over tasks (a.queue); without it each
-// wave runs its one task and the loop folds away (the task loop's live ranges cost the Riccati
-// sweeps ≈75 more spilled registers: config 3 61.4 → 65.7 ms, so only launches with more
-// blocks than the chip holds take the queue form, profiles/r4/r4z/).
+// wave runs its one task.  The task is a lambda called once or in the loop: written inline in
+// the loop, the loop's live ranges cost the sweeps ≈75 more spilled registers (config 4 76.2
+// ms, config 3 65.7); as a lambda the queue form spills 37–60 and runs config 4 in 72.3 ms,
+// at +1 % for config 3 (profiles/r4/r4z/, r4aa/).
 template <int S, int G, bool NT, bool RUNS, bool QUEUE>
 __global__ void __launch_bounds__(64 * G, 2)
     zmpc_strict_lq_kernel(LqArgs a, const double* __restrict__ tab) {
@@ -553,8 +554,8 @@ __global__ void __launch_bounds__(64 * G, 2)
   unsigned long long n_sb_ws = 0, n_sb_free = 0;
 #endif
   unsigned itmax = 0;  // most passes of one of this lane's solves (counter [8])
-  int64_t task = gw;   // this wave's (group, axis): gw's own first, then from the queue
-  for (;;) {
+  // one task: the rollout of one 64-walk group on one axis (this wave's lanes)
+  auto run_task = [&](const int64_t task) {
   // (the task's block and wave: the kernel's own without a queue)
   const int64_t tblk = QUEUE ? task / G : (int64_t)blockIdx.x;
   const int twave = QUEUE ? (int)(task % G) : wave;
@@ -793,8 +794,13 @@ __global__ void __launch_bounds__(64 * G, 2)
     else if (fq != 0)
       atomicOr(&a.status[b], fq);
   }
+  };
   if constexpr (QUEUE && G == 8) {
-    // the next task: one device-scope atomic per task (a task is a whole rollout of 64 walks)
+    // the wave's own task (gw), then the queue's: one device-scope atomic per task (a task is a
+    // whole rollout of 64 walks)
+    int64_t task = gw;
+    for (;;) {
+    run_task(task);
     int q = 0;
     if (lane == 0) q = atomicAdd(a.queue, 1);
     q = __builtin_amdgcn_readfirstlane(__shfl(q, 0, 64));
@@ -804,9 +810,9 @@ __global__ void __launch_bounds__(64 * G, 2)
     const int64_t qq = q < half ? q : q - half;
     const int64_t blk = a.qblock0 + qq / (G / 2);
     task = blk * G + (q < half ? G / 2 : 0) + qq % (G / 2);
+    }
   } else {
-    break;  // one task per wave (the host takes the queue form for 8-wave blocks only)
-  }
+    run_task(gw);  // one task per wave (the host takes the queue form for 8-wave blocks only)
   }
   if (a.cnt) {
     for (int o = 32; o > 0; o >>= 1) {
