@@ -59,10 +59,12 @@ FP64_SUSTAINED_TFS = 56.6  # profiles/r1_fp64_peak.log: register-only FMA chains
 SEED = 20251226
 SPARSE_MAX = 40  # rollout.hip kSparseMax: z_ref changes per axis the sparse correlation takes
 SPARSE_MAX_WIDE = 64  # kSparseMaxWide: the same for the wide kernel (walks > 513 samples)
-# strict_lq.hip FLOP per instance-slot of one active-set pass (fma = 2): working-set slot =
-# Riccati step 117 + forward 24 + costate 19; free-tail slot = s recursion 23 + forward 21
-STRICT_FLOP_WS = 160
-STRICT_FLOP_TAIL = 44
+# strict_lq.hip FLOP per instance-slot of one active-set pass (fma = 2, the z-input form of
+# strict_eta.h, round 5): working-set slot = Riccati step 70 (its shared part 22, 1/Quu 9, the
+# law 10, the P/s update 29) + forward 13 + costate and multiplier 13; free-tail slot = s
+# recursion 13 + forward 13.  (The v-input form of rounds 1-4 counted 160 and 44.)
+STRICT_FLOP_WS = 96
+STRICT_FLOP_TAIL = 26
 
 
 CONFIGS = {
@@ -193,7 +195,7 @@ def herdt_bench(args, rank, world, dev, dist_on):
                    "horizon": N, "samples_per_walk": n, "solves_per_step": solves_per_step,
                    "parallelism": f"dp{world}", "max_footsteps_in_window": mmax,
                    "solve": "one joint x/y QP (predict_herdt_joint, zmp_controller.py:533-826)"},
-        "roofline": {"bound": "mfma", "achieved": tfs, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
+        "roofline": {"bound": "fp64", "achieved": tfs, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s",
                      "frac": tfs / FP64_PEAK_TFS, "traffic": pmc_traffic(f"config6_n{N}_b{B}"),
                      "kernel": "zmpc_herdt_kernel", "kernel_ms": kern_ms,
                      "alg_flops_per_launch": flops,
@@ -889,23 +891,27 @@ def main():
         wide = n - 1 > 512  # wide kernel: its own limit, and a walk is sparse if both axes are
         lim = SPARSE_MAX_WIDE if wide else SPARSE_MAX
         sparse_frac = float((ch.max(axis=1) <= lim).mean() if wide else (ch <= lim).mean())
-        plan.set_option("correlation", 1)  # ZMPC_OPT_CORRELATION: dense forms only
-        try:
-            for _ in range(max(1, args.warmup)):
-                launch()
-            torch.cuda.synchronize()
-            _, dense_ms = timed_region(launch, args.steps, False, dev)
-        finally:
-            plan.set_option("correlation", 0)
-            launch()  # the history the rest of the run reads comes from the default form
-            torch.cuda.synchronize()
-        corr = {"form": "sparse-difference",
+        corr_opt = plan.get_option("correlation")  # (an --option correlation=1 run keeps it)
+        dense_ms = None
+        if corr_opt != 1:
+            plan.set_option("correlation", 1)  # ZMPC_OPT_CORRELATION: dense forms only
+            try:
+                for _ in range(max(1, args.warmup)):
+                    launch()
+                torch.cuda.synchronize()
+                _, dense_ms = timed_region(launch, args.steps, False, dev)
+            finally:
+                plan.set_option("correlation", corr_opt)
+                launch()  # the history the rest of the run reads comes from the run's form
+                torch.cuda.synchronize()
+        corr = {"form": "dense (option correlation=1)" if corr_opt == 1 else "sparse-difference",
                 "sparse_max_changes_per_axis": lim,
                 "zref_changes_per_axis_mean": float(ch.mean()),
                 "zref_changes_per_axis_max": int(ch.max()),
                 "sparse_frac": sparse_frac,
-                "dense_kernel_ms": dense_ms,
-                "dense_hbm_frac": alg_bytes / (dense_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}
+                "dense_kernel_ms": dense_ms if dense_ms is not None else kern_ms,
+                "dense_hbm_frac": alg_bytes / ((dense_ms if dense_ms is not None else kern_ms)
+                                               * 1e-3) / 1e9 / HBM_PEAK_GBS}
 
     gather_ms = None
     gather_ok = None
@@ -969,7 +975,7 @@ def main():
         elif not cfg.strict:
             # long horizons (config 5: 2N+20 = 1044 FLOP per solve) are FP64-bound; the
             # dtype's dense peak (78.6 TF, vector = matrix); the kernel runs on the VALU
-            roof = {"bound": "mfma", "achieved": fp64_tfs, "peak": FP64_PEAK_TFS,
+            roof = {"bound": "fp64", "achieved": fp64_tfs, "peak": FP64_PEAK_TFS,
                     "unit": "TFLOP/s", "frac": fp64_tfs / FP64_PEAK_TFS,
                     "engine": "FP64 VALU (v_mfma_f64 measured slower, DESIGN.md §4)"}
         else:
@@ -982,7 +988,7 @@ def main():
             ws = work["working_set_slots"]
             sflops = (ws * STRICT_FLOP_WS + (slots - ws) * STRICT_FLOP_TAIL) / per
             s_tf = sflops / (kern_ms * 1e-3) / 1e12
-            roof = {"bound": "mfma", "achieved": s_tf, "peak": FP64_PEAK_TFS,
+            roof = {"bound": "fp64", "achieved": s_tf, "peak": FP64_PEAK_TFS,
                     "unit": "TFLOP/s", "frac": s_tf / FP64_PEAK_TFS,
                     "engine": "FP64 VALU (one instance per lane; no MFMA-shaped work)",
                     "strict_alg_flops_per_launch": sflops,

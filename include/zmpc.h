@@ -229,12 +229,14 @@ typedef struct zmpc_herdt_params {
   int32_t max_footsteps;             /* most footsteps (support segments after the current
                                         one) inside any horizon window of the batch, <= 8 */
   int32_t max_passes;                /* active-set pass cap per joint QP (0: the default 64).
-                                        A solve that reaches it, or whose swing polytope is
-                                        infeasible, takes the reference's failure fallback
+                                        A solve that reaches it keeps its last iterate (as OSQP
+                                        returns its iterate at its own iteration limit) and sets
+                                        ZMPC_ST_MAXITER.  A solve whose swing polytope is
+                                        infeasible — the analogue of OSQP returning no solution
+                                        — takes the reference's failure fallback
                                         (zmp_controller.py:796-802: zero jerk on both axes, the
-                                        first footstep at the air foot's centre — the current
-                                        foot for zmpc_herdt_step) and sets ZMPC_ST_MAXITER /
-                                        ZMPC_ST_INFEASIBLE in the walk's status */
+                                        first footstep at the air foot's centre; the current
+                                        foot for zmpc_herdt_step) and sets ZMPC_ST_INFEASIBLE */
 } zmpc_herdt_params;
 
 /*

@@ -41,12 +41,12 @@
 
 namespace {
 
-constexpr int HMAXIT = 64;
+constexpr int HMAXIT = 64;  // default active-set pass cap (zmpc_herdt_params.max_passes)
 #ifdef ZMPC_DIAG
 constexpr bool kProf = true;  // per-phase clocks (ZMPC_HERDT_PROF), diagnostics build only
 #else
 constexpr bool kProf = false;
-#endif  // default active-set pass cap (zmpc_herdt_params.max_passes)
+#endif
 
 struct HerdtArgs {
   int N;
@@ -859,11 +859,12 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
     }
     if (valid) itmax = max(itmax, (unsigned)it);
     if (valid) pr_own += (unsigned long long)own;
-    // a failed joint QP (either lane of the pair) takes the reference's fallback
-    // (zmp_controller.py:796-802): zero jerk on both axes and the first footstep at the air
-    // foot's centre; the walk's status keeps the failure bit
+    // an infeasible joint QP (either lane of the pair) — the analogue of OSQP returning no
+    // solution — takes the reference's fallback (zmp_controller.py:796-802): zero jerk on both
+    // axes and the first footstep at the air foot's centre.  A solve at the pass cap keeps its
+    // last iterate, as OSQP does at its iteration limit.  The walk's status keeps both bits.
     fq |= fstep;
-    if ((fstep | __shfl_xor(fstep, 1, 64)) != 0) {
+    if (((fstep | __shfl_xor(fstep, 1, 64)) & ZMPC_ST_INFEASIBLE) != 0) {
       u0 = 0.0;
       if (m > 0) f0 = air;
     }

@@ -1061,8 +1061,8 @@ static int strict_mode(const zmpc_plan* p, int64_t ninst) {
   const bool scan_ok = zmpc_strict_scan_supported(p);
   if (opt == 1) return kTile;
   if (opt == 2) return kWave;
-  if (opt == 3 && lq_ok) return kLq;
-  if (opt == 4 && scan_ok) return kScan;
+  if (opt == 3) return kLq;    // (zmpc_plan_set_option accepts 3 and 4 only where they run)
+  if (opt == 4) return kScan;
   if (scan_ok && (ninst <= kScanMaxInst || !lq_ok)) return kScan;
   return lq_ok ? kLq : kTile;
 }

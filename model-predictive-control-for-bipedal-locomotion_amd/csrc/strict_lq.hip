@@ -16,14 +16,16 @@
 // Coordinates.  ξ = [x0, T x1, T² x2], v = T³ u, objective divided by Q, and then
 //   η = [ξ0 − ξ2/6, ξ1 − ξ2/2, ξ2]:   η⁺ = Ā η + e2 v,   Ā = [[1,1,1],[0,1,1],[0,0,1]],
 //   z = c̄ᵀη + π v,  c̄ = [1, 1, γ'],  γ' = 7/6 − (h/g)/T²,  π = 1/6 − (h/g)/T² (= p(0)/T³),
-// stage cost ½(z − r)² + ½ρv², ρ = R/(Q T⁶).  With the input on the last state alone (B̄ = e2)
-// the Riccati step needs no B-products at all (B̄ᵀPB̄ = P22, PB̄ = P[:,2], B̄ᵀs = s2) and ĀᵀPĀ is
-// the 2-D prefix sum of P: 44 FP64 operations for a free slot and 57 for the branch-free
-// working-set form (the previous ξ-coordinate kernel: 62 and 75).  Value function
-// V(η) = ½ηᵀPη − sᵀη; a slot's law v = −K η − kff:
-//   free:    K = Qux/Quu, kff = qu/Quu;  pinned at t: K = c̄/π, kff = −t/π
-//   P ← c̄c̄ᵀ + ĀᵀPĀ − Qux Kᵀ + K Dᵀ,  s ← −qx + K qu − kff D,  D = Quu K − Qux (0 when free)
-//   Qux = π c̄ + e2ᵀPĀ,  Quu = π² + ρ + P22,  qu = −(π r + s2),  −qx = r c̄ + Āᵀs.
+// stage cost ½(z − r)² + ½ρv², ρ = R/(Q T⁶).  The Riccati step takes the slot's ZMP z itself
+// as the input (v = (z − c̄ᵀη)/π, strict_eta.h): a pinned slot is then z = t exactly (K = 0,
+// kff = −t), and the value-function update has no cancellation at any weight (round 5: the
+// v-input form lost three digits at R/Q = 1e-9).  Value function V(η) = ½ηᵀPη − sᵀη; a slot's
+// law z = −K η − kff:
+//   free:    K = Qux/Quu, kff = qu/Quu;  pinned at t: K = 0, kff = −t
+//   P ← Qxx − Qux Kᵀ,  s ← Fᵀs + Qux kff,  F = Ā − e2 c̄ᵀ/π,
+//   Qux = FᵀPe2/π − ε c̄,  Quu = 1 + ε + P22/π²,  qu = −(r + s2/π),  Qxx = ε c̄c̄ᵀ + FᵀPF,
+// ε = ρ/π²; F's last two columns are equal and ĀᵀPĀ-style prefix sums give FᵀPF: ≈48 FP64
+// operations for the branch-free working-set step (57 in the v-input form).
 // oracle/strict_lq_cpu.c restates the same algorithm in C (the checker and the optimized CPU
 // baseline).
 //
@@ -67,7 +69,8 @@ constexpr int LQ_DRIFT = ZMPC_LQ_DRIFT;  // timesteps a lane may run ahead of it
                               // (round 3, profiles/r3u/, r3drift/: 0/1/2/4/8 → 104.5/94.8/92.5/
                               // 90.9/92.7 ms at config 3 — the bound rows stay a few rows apart)
 constexpr int TAB = 16;       // doubles per slot of the free-tail table: [0..2] K, [3] 1/Quu,
-                              // [4..9] P after the slot (V_k: slots k..N−1 free), padding
+                              // [4..9] P after the slot (V_k: slots k..N−1 free), [10..12] Qux,
+                              // padding
 
 struct LqArgs {
   int N, NS;             // horizon, segments ⌈N/S⌉
@@ -101,11 +104,9 @@ struct LqArgs {
   unsigned long long* cnt;  // plan work counters (zmpc_plan_counters), may be null
   double T, T2, T3;      // reference-form state advance (zmp_controller.py:18-20,199)
   double Tsq, Tcu;       // T², T³ (coordinate scaling)
-  double pi, ipi;        // π, 1/π
-  double gp, gp2, gipi;  // γ', γ'², γ'/π
-  double pig;            // π γ'
-  double rho, quu0;      // ρ, π² + ρ
-  double tolnu;          // multiplier tolerance in the scaled objective (1e-13 / Q)
+  // z-form step constants (strict_eta.h fill_eta): π, 1/π, 1/π², γ', ρ, ε = ρ/π², εγ', εγ'²,
+  // 1 + ε, ρ/π, and the multiplier tolerance (metres, 1e-13)
+  double pi, ipi, ipi2, gp, rho, eps, epsg, epsg2, quz0, epi, tolnu;
   // task queue (rollouts with more waves than the chip holds): the grid is the resident
   // blocks; each wave runs its own task first (gw), then takes the next from *queue:
   // queue index q → the remaining blocks' y waves first (the heavier axis), then their x
@@ -124,47 +125,20 @@ struct SegIn {  // a segment's window slots: z_ref, half-width of the box, worki
 template <int S>
 struct SegOut {  // a segment's feedback (v = −K η − kff) and forward outputs, per step
   double K0[S], K1[S], K2[S], kf[S];
-  double w[S];  // forward: z_k − r_k at free slots, v_k at pinned slots
+  double w[S];  // forward: v_k (= T³u_k)
   int nf[S];    // forward: the free slots' primal verdict (0 stays free, ±1 violated)
 };
 
-// The same step for a free slot (ric_step with f = 0 and D = 0 folded: identical values up to
-// the sign of a zero).  Also returns 1/Quu (the free-tail table).
-__device__ __forceinline__ void ric_free(const LqArgs& a, Ric& v, double r, double& K0,
-                                         double& K1, double& K2, double& kf, double& iqo) {
-  const StepCore c = step_core(a, v, r);
-  const double iq = recip(c.Quu);
-  K0 = c.ux0 * iq;
-  K1 = c.ux1 * iq;
-  K2 = c.ux2 * iq;
-  kf = -c.w * iq;
-  iqo = iq;
-  const double P00 = fma(-c.ux0, K0, 1.0 + v.p00);
-  const double P01 = fma(-c.ux0, K1, 1.0 + c.m01);
-  const double P02 = fma(-c.ux0, K2, a.gp + c.m02);
-  const double P11 = fma(-c.ux1, K1, 1.0 + c.m11);
-  const double P12 = fma(-c.ux1, K2, a.gp + c.m12);
-  const double P22 = fma(-c.ux2, K2, a.gp2 + c.m22);
-  v.s0 = fma(-K0, c.w, c.nqx0);
-  v.s1 = fma(-K1, c.w, c.nqx1);
-  v.s2 = fma(-K2, c.w, c.nqx2);
-  v.p00 = P00;
-  v.p01 = P01;
-  v.p02 = P02;
-  v.p11 = P11;
-  v.p12 = P12;
-  v.p22 = P22;
-}
-
-// A free-tail step: P, K and 1/Quu come from the table, only s moves (ric_free's s update).
-__device__ __forceinline__ void ric_tail(const LqArgs& a, Ric& v, double r, double K0, double K1,
-                                         double K2, double iq, double& kf) {
-  const double w = fma(a.pi, r, v.s2);
-  const double t1 = v.s0 + v.s1, t2 = t1 + v.s2;
-  kf = -w * iq;
-  v.s0 = fma(-K0, w, r + v.s0);
-  v.s1 = fma(-K1, w, r + t1);
-  v.s2 = fma(-K2, w, fma(a.gp, r, t2));
+// A free-tail step: P, K, Qux and 1/Quu come from the table, only s moves (strict_eta.h's
+// s ← Fᵀs + Qux kff with kff = −(r + s2/π)/Quu).
+__device__ __forceinline__ void ric_tail(const LqArgs& a, Ric& v, double r, double u0, double u1,
+                                         double u2, double iq, double& kf) {
+  kf = -fma(a.ipi, v.s2, r) * iq;
+  const double as2 = a.ipi * v.s2;
+  const double f0 = v.s0 - as2, f1 = (v.s0 + v.s1) - as2;
+  v.s0 = fma(u0, kf, f0);
+  v.s1 = fma(u1, kf, f1);
+  v.s2 = fma(u2, kf, f1);
 }
 
 struct Lane {
@@ -324,8 +298,8 @@ __device__ __forceinline__ void seg_riccati(const LqArgs& a, int j, Ric& v, cons
     if (FULL || k < a.N) {
       double K0, K1, K2, kf;
       if (FREE) {
-        double iq;
-        ric_free(a, v, in.r[q], K0, K1, K2, kf, iq);
+        double iq, u0, u1, u2;
+        ric_free(a, v, in.r[q], K0, K1, K2, kf, iq, u0, u1, u2);
       } else {
         ric_step(a, v, in.r[q], in.h[q], in.f[q], K0, K1, K2, kf);
       }
@@ -353,7 +327,7 @@ __device__ __forceinline__ void seg_tail(const LqArgs& a, const double* __restri
     if (FULL || k < a.N) {
       const double* t = tab + (size_t)k * TAB;
       double kf;
-      ric_tail(a, v, in.r[q], t[0], t[1], t[2], t[3], kf);
+      ric_tail(a, v, in.r[q], t[10], t[11], t[12], t[3], kf);
       if (KEEP) g.kf[q] = kf;
     }
   }
@@ -373,7 +347,7 @@ __device__ __forceinline__ void seg_forward(const LqArgs& a, int j, const SegIn<
       fwd_step(a, g.K0[q], g.K1[q], g.K2[q], g.kf[q], x, u, z);
       if (k == 0) u0 = u;
       const double d = z - in.r[q], ht = in.h[q] + tol;
-      g.w[q] = (in.f[q] == 0) ? d : u;
+      g.w[q] = u;
       g.nf[q] = (d > ht) ? 1 : ((d < -ht) ? -1 : 0);
     }
   }
@@ -404,9 +378,9 @@ __device__ __forceinline__ void seg_forward_tail(const LqArgs& a, const double* 
   }
 }
 
-// Costate sweep back through segment j from λ at its end (λ_k = ∇V_k(η_k) = c̄ e_k + Āᵀλ_{k+1},
-// e_k = z_k − r_k + ν_k): the bound multipliers ν_k of the pinned slots, dual check, the slot's
-// new flag; kl = the last slot pinned in the new set.
+// Costate sweep back through segment j from λ at its end (λ_k = ∇V_k(η_k) = Fᵀλ_{k+1} − επ v_k c̄,
+// strict_eta.h): the bound multipliers ν_k of the pinned slots, dual check, the slot's new flag;
+// kl = the last slot pinned in the new set.
 template <int S, bool FULL>
 __device__ __forceinline__ void seg_costate(const LqArgs& a, int j, const SegIn<S>& in,
                                             const SegOut<S>& g, double* lam, bool& changed,
@@ -416,11 +390,9 @@ __device__ __forceinline__ void seg_costate(const LqArgs& a, int j, const SegIn<
     const int k = j * S + q;
     if (FULL || k < a.N) {
       const int f = in.f[q];
-      // pinned: π e + ρ v + λ2_{k+1} = 0 (stationarity in v_k; B̄ᵀλ = λ2)
-      const double e = (f == 0) ? g.w[q] : -fma(a.rho, g.w[q], lam[2]) * a.ipi;
       {
         const double sg = (double)f;
-        const double nu = fma(-sg, in.h[q], e);  // e − (t − r): ν / Q (pinned slots only)
+        const double nu = pinned_nu(a, sg, in.h[q], g.w[q], lam);  // ν / Q (pinned slots only)
         // wrong-signed multiplier (ν < 0 at z_max, ν > 0 at z_min): σν < −tol; free: 0 < −tol
         const bool rel = sg * nu < -a.tolnu;
         // the slot's new flag, written unconditionally (branch-free)
@@ -429,11 +401,7 @@ __device__ __forceinline__ void seg_costate(const LqArgs& a, int j, const SegIn<
         changed |= nf != f;
         kl = (nf != 0 && k > kl) ? k : kl;
       }
-      const double s01 = lam[0] + lam[1];
-      const double s012 = s01 + lam[2];
-      lam[0] = e + lam[0];
-      lam[1] = e + s01;
-      lam[2] = fma(a.gp, e, s012);
+      costate_step(a, g.w[q], lam);
     }
   }
 }
@@ -840,8 +808,8 @@ __global__ void zmpc_strict_lq_table_kernel(LqArgs a, double* tab) {
   if (threadIdx.x != 0 || blockIdx.x != 0) return;
   Ric v{0, 0, 0, 0, 0, 0, 0, 0, 0};
   for (int k = a.N - 1; k >= 0; --k) {
-    double K0, K1, K2, kf, iq;
-    ric_free(a, v, 0.0, K0, K1, K2, kf, iq);
+    double K0, K1, K2, kf, iq, u0, u1, u2;
+    ric_free(a, v, 0.0, K0, K1, K2, kf, iq, u0, u1, u2);
     double* t = tab + (size_t)k * TAB;
     t[0] = K0;
     t[1] = K1;
@@ -853,7 +821,10 @@ __global__ void zmpc_strict_lq_table_kernel(LqArgs a, double* tab) {
     t[7] = v.p11;
     t[8] = v.p12;
     t[9] = v.p22;
-    for (int c = 10; c < TAB; ++c) t[c] = 0.0;
+    t[10] = u0;
+    t[11] = u1;
+    t[12] = u2;
+    for (int c = 13; c < TAB; ++c) t[c] = 0.0;
   }
 }
 
@@ -1007,18 +978,7 @@ void fill_consts(const zmpc_plan* p, LqArgs& a) {
   a.T = p->T;
   a.T2 = p->T2_2;
   a.T3 = p->T3_6;
-  a.Tsq = p->T * p->T;
-  a.Tcu = a.Tsq * p->T;
-  const double hgt = p->hg / a.Tsq;
-  a.pi = 1.0 / 6.0 - hgt;  // p(0)/T³ (zmp_controller.py:171, i = j)
-  a.ipi = 1.0 / a.pi;
-  a.gp = 7.0 / 6.0 - hgt;
-  a.gp2 = a.gp * a.gp;
-  a.gipi = a.gp / a.pi;
-  a.pig = a.pi * a.gp;
-  a.rho = p->R / (p->Q * a.Tcu * a.Tcu);
-  a.quu0 = a.pi * a.pi + a.rho;
-  a.tolnu = 1e-13 / p->Q;
+  fill_eta(a, p->T, p->hg, p->Q, p->R);
   a.cnt = p->lqcnt;
 }
 

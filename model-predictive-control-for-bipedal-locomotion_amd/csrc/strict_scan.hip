@@ -13,7 +13,8 @@
 //             (J, g) part of the lane's right neighbour's suffix is the value function
 //             V(η) = ½ηᵀJη − gᵀη at the chunk's end: each lane then runs the ordinary Riccati
 //             step (ric_step) back through its own C slots;
-//   forward   each lane composes its slots' closed-loop maps η⁺ = (Ā − e2Kᵀ)η − e2 kff into one
+//   forward   each lane composes its slots' closed-loop maps (z = −Kη − kff, η⁺ = Fη + e2 z/π,
+//             strict_eta.h) into one
 //             affine map, a prefix scan over the lanes gives the state at every chunk's start,
 //             and each lane rolls through its slots: primal check of the free slots, the pinned
 //             slots' multipliers from ∇V_{k+1}(η_{k+1}) (the costate), the new working set.
@@ -58,9 +59,9 @@ struct ScanArgs {
   int32_t* status;
   unsigned long long* cnt;
   double T, T2, T3, Tsq, Tcu;  // reference-form advance, coordinate scaling
-  // η-step constants (strict_eta.h)
-  double pi, ipi, gipi, pig, gp, gp2, quu0, rho, tolnu;
-  double iR, piR, rhoR, rhoP2;  // 1/R, π/R, ρ/R, ρ/π²
+  // z-form step constants (strict_eta.h fill_eta)
+  double pi, ipi, ipi2, gp, rho, eps, epsg, epsg2, quz0, epi, tolnu;
+  double iR, piR, rhoR, rhoP2;  // slot elements: 1/R, π/R, ρ/R, ρ/π² (R = π² + ρ)
 };
 
 // symmetric 3×3 in 6 doubles: 00 01 02 11 12 22
@@ -317,7 +318,8 @@ __global__ void __launch_bounds__(64, 2) zmpc_strict_scan_kernel(ScanArgs a) {
 #pragma unroll
   for (int q = 0; q < C; ++q) f[q] = 0;
   int fq = 0;
-  unsigned long long passes = 0;
+  unsigned long long passes = 0;   // the instance's passes (counters [1], [2])
+  unsigned long long wpasses = 0;  // the wave's passes: per timestep the most of its instances
   unsigned itmax = 0;
   const unsigned long long imask = (L == 64) ? ~0ull : (((1ull << L) - 1) << base);
 
@@ -425,19 +427,22 @@ __global__ void __launch_bounds__(64, 2) zmpc_strict_scan_kernel(ScanArgs a) {
       for (int q = 0; q < C; ++q) {
         if (k0 + q < N) {
 #pragma unroll
-          for (int c = 0; c < 3; ++c) {  // column c of F through η⁺ = Āη − e2(Kᵀη)
+          // column c of F through η⁺: η0⁺ = η0 + η1 + η2, η1⁺ = η1 + η2, η2⁺ = (z − η0⁺)/π
+          for (int c = 0; c < 3; ++c) {
             const double y0 = F[c], y1 = F[3 + c], y2 = F[6 + c];
             const double kv2 = fma(K0[q], y0, fma(K1[q], y1, K2[q] * y2));
             const double s12 = y1 + y2;
-            F[c] = y0 + s12;
+            const double e0 = y0 + s12;
+            F[c] = e0;
             F[3 + c] = s12;
-            F[6 + c] = y2 - kv2;
+            F[6 + c] = -a.ipi * (kv2 + e0);
           }
           const double kv2 = fma(K0[q], ph[0], fma(K1[q], ph[1], K2[q] * ph[2])) + kf[q];
           const double s12 = ph[1] + ph[2];
-          ph[0] = ph[0] + s12;
+          const double e0 = ph[0] + s12;
+          ph[0] = e0;
           ph[1] = s12;
-          ph[2] = ph[2] - kv2;
+          ph[2] = -a.ipi * (kv2 + e0);
         }
       }
 #pragma unroll
@@ -489,7 +494,7 @@ __global__ void __launch_bounds__(64, 2) zmpc_strict_scan_kernel(ScanArgs a) {
           lam[i2] = il == L - 1 ? 0.0 : dn;
         }
       }
-      double wv[C];  // z − r at a free slot, v at a pinned one (strict_lq.hip seg_forward)
+      double wv[C];  // v (= T³u) at every slot (strict_lq.hip seg_forward)
       int np[C];     // a free slot's primal verdict
       const double tol = 1e-13;  // as strict_lq.hip
 #pragma unroll
@@ -501,7 +506,7 @@ __global__ void __launch_bounds__(64, 2) zmpc_strict_scan_kernel(ScanArgs a) {
           fwd_step(a, K0[q], K1[q], K2[q], kf[q], xs, vq, z);
           if (k0 + q == 0 && mine) v0 = vq;
           const double d = z - r[q], ht = h[q] + tol;
-          wv[q] = (f[q] == 0) ? d : vq;
+          wv[q] = vq;
           np[q] = (d > ht) ? 1 : ((d < -ht) ? -1 : 0);
         }
       }
@@ -512,19 +517,13 @@ __global__ void __launch_bounds__(64, 2) zmpc_strict_scan_kernel(ScanArgs a) {
       for (int q = C - 1; q >= 0; --q) {
         if (k0 + q < N) {
           const int fl = f[q];
-          // pinned: π e + ρ v + λ2_{k+1} = 0 (stationarity in v_k)
-          const double e = (fl == 0) ? wv[q] : -fma(a.rho, wv[q], lam[2]) * a.ipi;
           const double sg = (double)fl;
-          const double nu = fma(-sg, h[q], e);  // e − (t − r): ν / Q at pinned slots
+          const double nu = pinned_nu(a, sg, h[q], wv[q], lam);  // ν / Q at pinned slots
           const bool rel = sg * nu < -a.tolnu;
           const int nf = (fl == 0) ? np[q] : (rel ? 0 : fl);
           changed |= nf != fl;
           if (mine) f[q] = nf;
-          const double s01 = lam[0] + lam[1];
-          const double s012 = s01 + lam[2];
-          lam[0] = e + lam[0];
-          lam[1] = e + s01;
-          lam[2] = fma(a.gp, e, s012);
+          costate_step(a, wv[q], lam);
         }
       }
       // the instance's verdict (its L lanes of the wave's ballot)
@@ -542,6 +541,11 @@ __global__ void __launch_bounds__(64, 2) zmpc_strict_scan_kernel(ScanArgs a) {
     }
     passes += (unsigned long long)it;
     itmax = max(itmax, (unsigned)it);
+    {
+      int wit = it;  // (lanes of one instance hold the same count)
+      for (int o = L; o < 64; o <<= 1) wit = max(wit, __shfl_xor(wit, o, 64));
+      wpasses += (unsigned long long)wit;
+    }
     // converged: advance in the reference form x⁺ = A x + B u0 (zmp_controller.py:199)
     const double u0 = __shfl(v0, base, 64) / a.Tcu;
     double xn[3];
@@ -581,7 +585,7 @@ __global__ void __launch_bounds__(64, 2) zmpc_strict_scan_kernel(ScanArgs a) {
         atomicOr(&a.status[b], fq);
     }
     if (a.cnt) {
-      atomicAdd(a.cnt + 0, passes);
+      if (lane == 0) atomicAdd(a.cnt + 0, wpasses);  // once per wave
       atomicAdd(a.cnt + 1, passes);
       atomicAdd(a.cnt + 2, passes * (unsigned long long)N);
       atomicMax(a.cnt + 8, (unsigned long long)itmax);
@@ -589,27 +593,23 @@ __global__ void __launch_bounds__(64, 2) zmpc_strict_scan_kernel(ScanArgs a) {
   }
 }
 
+// The kernel's constants from (T, the reference-form advance's T²/2 and T³/6, h/g, Q, R); also
+// called by tests/emu's host build of this kernel.
+void fill_consts(ScanArgs& a, double T, double T2_2, double T3_6, double hg, double Q, double R) {
+  a.T = T;
+  a.T2 = T2_2;
+  a.T3 = T3_6;
+  fill_eta(a, T, hg, Q, R);
+  const double quu = a.pi * a.pi + a.rho;  // the slot elements' R (v-input form, header)
+  a.iR = 1.0 / quu;
+  a.piR = a.pi / quu;
+  a.rhoR = a.rho / quu;
+  a.rhoP2 = a.rho * a.ipi2;
+}
+
 void fill(const zmpc_plan* p, ScanArgs& a) {
   a.N = p->N;
-  a.T = p->T;
-  a.T2 = p->T2_2;
-  a.T3 = p->T3_6;
-  a.Tsq = p->T * p->T;
-  a.Tcu = a.Tsq * p->T;
-  const double hgt = p->hg / a.Tsq;
-  a.pi = 1.0 / 6.0 - hgt;
-  a.ipi = 1.0 / a.pi;
-  a.gp = 7.0 / 6.0 - hgt;
-  a.gp2 = a.gp * a.gp;
-  a.gipi = a.gp / a.pi;
-  a.pig = a.pi * a.gp;
-  a.rho = p->R / (p->Q * a.Tcu * a.Tcu);
-  a.quu0 = a.pi * a.pi + a.rho;
-  a.tolnu = 1e-13 / p->Q;
-  a.iR = 1.0 / a.quu0;
-  a.piR = a.pi / a.quu0;
-  a.rhoR = a.rho / a.quu0;
-  a.rhoP2 = a.rho / (a.pi * a.pi);
+  fill_consts(a, p->T, p->T2_2, p->T3_6, p->hg, p->Q, p->R);
   a.cnt = p->lqcnt;
 }
 

@@ -56,9 +56,10 @@ class ZMPController:
     def _herdt_status(self, status):
         """Herdt drop-ins: the reference never raises on a failed joint QP — it prints a message,
         substitutes zero jerk and the air foot's centre and continues (zmp_controller.py:796-802).
-        The kernel applies that same fallback to a solve that reached the active-set pass cap
-        (ZMPC_ST_MAXITER) or whose swing polytope is infeasible (ZMPC_ST_INFEASIBLE), so those
-        print the reference's message (and warn); any other flag (non-finite state, footstep
+        The kernel applies that same fallback to a solve whose swing polytope is infeasible
+        (ZMPC_ST_INFEASIBLE, the analogue of OSQP returning no solution); a solve that reached the
+        active-set pass cap (ZMPC_ST_MAXITER) keeps its last iterate, as OSQP returns its iterate
+        at its own iteration limit.  Both warn; any other flag (non-finite state, footstep
         factorisation, more footsteps than the kernel was built for) raises RuntimeError."""
         st = status.cpu().numpy() if isinstance(status, torch.Tensor) else np.asarray(status)
         soft = _ST_MAXITER | _ST_INFEASIBLE
@@ -66,9 +67,9 @@ class ZMPController:
             raise RuntimeError(_FAILED)
         if st.size and np.any(st & soft):
             msg = (f"Joint QP solver failed in {int(np.count_nonzero(st & soft))} walk(s) "
-                   f"(pass cap: {int(np.count_nonzero(st & _ST_MAXITER))}, infeasible swing "
-                   f"polytope: {int(np.count_nonzero(st & _ST_INFEASIBLE))}); zero jerk and the "
-                   f"air foot's centre were used for those solves")
+                   f"(pass cap, last iterate kept: {int(np.count_nonzero(st & _ST_MAXITER))}; "
+                   f"infeasible swing polytope, zero jerk and the air foot's centre used: "
+                   f"{int(np.count_nonzero(st & _ST_INFEASIBLE))})")
             print(msg)
             warnings.warn(msg, RuntimeWarning, stacklevel=3)
 
@@ -165,10 +166,10 @@ class ZMPController:
     def predict_herdt_joint(self, x_init, y_init, v_ref, x_fc, y_fc, current_state, state_ref,
                             nb_steps, nb_steps_to_next_state, x_airc, y_airc, foot_side, idx):
         """One joint x/y step (zmp_controller.py:533-826): (next x state (3,1), next y state
-        (3,1), first planned x footstep or None, first planned y footstep or None).  A solve that
-        fails (active-set pass cap, infeasible swing polytope) takes the reference's fallback
-        (:796-802): zero jerk (the kernel) and the air foot's centre x_airc / y_airc as the first
-        footstep (here; the C-ABI step knows only the current foot)."""
+        (3,1), first planned x footstep or None, first planned y footstep or None).  A solve whose
+        swing polytope is infeasible takes the reference's fallback (:796-802): zero jerk (the
+        kernel) and the air foot's centre x_airc / y_airc as the first footstep (here; the C-ABI
+        step knows only the current foot); one at the pass cap keeps its last iterate."""
         plan = self._plan(nb_steps)
         v = np.asarray(v_ref, np.float64).reshape(1, nb_steps, 2)
         win = herdt.encode_states(state_ref).reshape(1, nb_steps)
@@ -182,7 +183,7 @@ class ZMPController:
         side = np.array([0 if foot_side == "left" else 1], np.int8)
         xn, step, st = plan.herdt_step(prm, x, v, win, cur, foot, side)
         self._herdt_status(st)
-        failed = int(st[0]) & (_ST_MAXITER | _ST_INFEASIBLE)
+        failed = int(st[0]) & _ST_INFEASIBLE
         xn, step = xn[0].cpu().numpy(), step[0].cpu().numpy()
         fx = None if np.isnan(step[0]) else float(step[0])
         fy = None if np.isnan(step[1]) else float(step[1])

@@ -60,16 +60,35 @@ def qp_solve(Q, p, G=None, h=None, maxit=10000, tol=1e-12):
         uplus = np.append(u, 0.0)
         while True:
             nj = G[j]
+            # the step directions in the Q metric: r = S⁻¹NᵀQ⁻¹nj, S = NᵀQ⁻¹N by a Cholesky of S
+            # while it is well conditioned, else (consecutive ZMP rows nearly parallel) from a
+            # Householder QR of L⁻¹N, which stays accurate where S loses its digits
+            b = np.linalg.solve(L, nj)
             if act:
-                N = G[act].T                      # n × q
-                QiN = qinv(N)
-                S = N.T @ QiN                     # q × q
-                Qin = qinv(nj)
-                r = np.linalg.solve(S, N.T @ Qin)
-                z = Qin - QiN @ r
+                Bm = np.linalg.solve(L, G[act].T)     # L⁻¹N, n × q
+                c = Bm.T @ b
+                Ls = None
+                try:
+                    Ls = np.linalg.cholesky(Bm.T @ Bm)
+                    dg = np.diag(Ls)
+                    if dg.min() < 1e-6 * dg.max():
+                        Ls = None
+                except np.linalg.LinAlgError:
+                    Ls = None
+                if Ls is not None:
+                    r = np.linalg.solve(Ls.T, np.linalg.solve(Ls, c))
+                    zb = b - Bm @ r
+                else:
+                    U, Rf = np.linalg.qr(Bm)
+                    cu = U.T @ b
+                    r = np.linalg.solve(Rf, cu)        # N⁺-coefficients of nj
+                    zb = b - U @ cu
             else:
                 r = np.zeros(0)
-                z = qinv(nj)
+                zb = b
+            if np.linalg.norm(zb) <= 1e-13 * np.linalg.norm(b):
+                zb = np.zeros_like(zb)                # nj depends on the active normals
+            z = np.linalg.solve(L.T, zb)
             # dual step length (drop a constraint whose multiplier hits zero first)
             t1, k_drop = np.inf, -1
             for i in range(len(act)):

@@ -36,11 +36,13 @@ typedef struct {
   int N;
   double T, T2_2, T3_6;  // reference-form state advance (zmp_controller.py:18-20,199)
   double Tsq, Tcu;       // T², T³
-  double pi, ipi;        // π, 1/π
-  double gp, gp2, gipi;  // γ', γ'², γ'/π
-  double pig;            // π γ'
-  double rho, quu0;      // ρ, π² + ρ
-  double tolnu;          // multiplier tolerance in the scaled objective (1e-13 / Q)
+  double pi, ipi, ipi2;  // π, a = 1/π, a²
+  double gp;             // γ'
+  double rho, eps;       // ρ, ε = ρ/π²
+  double epsg, epsg2;    // εγ', εγ'²
+  double quz0;           // 1 + ε
+  double epi;            // επ = ρ/π
+  double tolnu;          // multiplier tolerance (metres of ZMP in the objective / Q)
 } Consts;
 
 typedef struct {
@@ -58,57 +60,56 @@ static void consts_init(Consts* c, int N, double T, double T2_2, double T3_6, do
   const double hgt = hg / c->Tsq;
   c->pi = 1.0 / 6.0 - hgt;
   c->ipi = 1.0 / c->pi;
+  c->ipi2 = c->ipi * c->ipi;
   c->gp = 7.0 / 6.0 - hgt;
-  c->gp2 = c->gp * c->gp;
-  c->gipi = c->gp / c->pi;
-  c->pig = c->pi * c->gp;
   c->rho = R / (Q * c->Tcu * c->Tcu);
-  c->quu0 = c->pi * c->pi + c->rho;
-  c->tolnu = 1e-13 / Q;
+  c->eps = c->rho * c->ipi2;
+  c->epsg = c->eps * c->gp;
+  c->epsg2 = c->epsg * c->gp;
+  c->quz0 = 1.0 + c->eps;
+  c->epi = c->rho * c->ipi;
+  c->tolnu = 1e-13;
 }
 
 // One backward Riccati step at a slot with flag f (0 free, 1 at z_max, 2 at z_min): V_{k+1} in v
-// -> V_k; the step's law v = −K η − kf.
+// -> V_k; the step's law z = −K η − kf, the slot's ZMP z as the input (z-control form: η⁺ = F η +
+// a e2 z, F = Ā − a e2 c̄ᵀ, stage ½(z − r)² + ½ε(z − c̄ᵀη)²; pinned: K = 0, kf = −t).
 static void ric_step(const Consts* c, Ric* v, double hi, double lo, int f, double K[3],
                      double* kf) {
-  const double q1 = v->p02 + v->p12, q2 = q1 + v->p22;
-  const double m01 = v->p00 + v->p01;
-  const double m11 = m01 + (v->p01 + v->p11);
-  const double m02 = m01 + v->p02, m12 = m11 + q1, m22 = m12 + q2;
-  const double ux0 = c->pi + v->p02, ux1 = c->pi + q1, ux2 = c->pig + q2;  // Qux
-  const double Quu = c->quu0 + v->p22;
   const double r = (hi + lo) / 2;  // z_ref (zmp_controller.py:184)
-  const double w = fma(c->pi, r, v->s2);  // −qu
-  const double t1 = v->s0 + v->s1, t2 = t1 + v->s2;
-  const double nqx0 = r + v->s0, nqx1 = r + t1, nqx2 = fma(c->gp, r, t2);  // −qx
-  double D0 = 0, D1 = 0, D2 = 0;
+  const double q1 = v->p02 + v->p12;
+  const double n01 = v->p00 + v->p01;
+  const double n11 = n01 + (v->p01 + v->p11);
+  const double w0 = c->ipi * v->p02, w1 = c->ipi * q1;
+  const double cc = c->ipi2 * v->p22;
+  const double ce = cc + c->eps, cg = cc + c->epsg;
+  const double u0 = w0 - ce, u1 = w1 - ce, u2 = w1 - cg;  // Qux
+  const double wz = fma(c->ipi, v->s2, r);                // −qu
   if (f == 0) {
-    const double iq = 1.0 / Quu;
-    K[0] = ux0 * iq;
-    K[1] = ux1 * iq;
-    K[2] = ux2 * iq;
-    *kf = -w * iq;
+    const double iq = 1.0 / (c->quz0 + cc);
+    K[0] = u0 * iq;
+    K[1] = u1 * iq;
+    K[2] = u2 * iq;
+    *kf = -wz * iq;
   } else {
-    const double t = (f == 1) ? hi : lo;
-    K[0] = c->ipi;
-    K[1] = c->ipi;
-    K[2] = c->gipi;
-    *kf = -t * c->ipi;
-    D0 = fma(Quu, K[0], -ux0);
-    D1 = fma(Quu, K[1], -ux1);
-    D2 = fma(Quu, K[2], -ux2);
+    K[0] = K[1] = K[2] = 0.0;
+    *kf = -((f == 1) ? hi : lo);
   }
-  // P = c̄c̄ᵀ + ĀᵀPĀ − Qux Kᵀ + K Dᵀ,  s = −qx + K qu − kf D
-  v->p00 = fma(K[0], D0, fma(-ux0, K[0], 1.0 + v->p00));
-  v->p01 = fma(K[0], D1, fma(-ux0, K[1], 1.0 + m01));
-  v->p02 = fma(K[0], D2, fma(-ux0, K[2], c->gp + m02));
-  v->p11 = fma(K[1], D1, fma(-ux1, K[1], 1.0 + m11));
-  v->p12 = fma(K[1], D2, fma(-ux1, K[2], c->gp + m12));
-  v->p22 = fma(K[2], D2, fma(-ux2, K[2], c->gp2 + m22));
-  const double f0 = *kf;
-  v->s0 = fma(-f0, D0, fma(-K[0], w, nqx0));
-  v->s1 = fma(-f0, D1, fma(-K[1], w, nqx1));
-  v->s2 = fma(-f0, D2, fma(-K[2], w, nqx2));
+  const double t00 = fma(-2.0, w0, v->p00);
+  const double t01 = (n01 - w0) - w1;
+  const double t11 = fma(-2.0, w1, n11);
+  // P = Qxx − Qux Kᵀ,  s = Fᵀs + Qux kf
+  v->p00 = fma(-u0, K[0], t00 + ce);
+  v->p01 = fma(-u0, K[1], t01 + ce);
+  v->p02 = fma(-u0, K[2], t01 + cg);
+  v->p11 = fma(-u1, K[1], t11 + ce);
+  v->p12 = fma(-u1, K[2], t11 + cg);
+  v->p22 = fma(-u2, K[2], t11 + (cc + c->epsg2));
+  const double as2 = c->ipi * v->s2;
+  const double f0 = v->s0 - as2, f1 = (v->s0 + v->s1) - as2;
+  v->s0 = fma(u0, *kf, f0);
+  v->s1 = fma(u1, *kf, f1);
+  v->s2 = fma(u2, *kf, f1);
 }
 
 typedef struct {
@@ -148,42 +149,43 @@ static int instance(const Consts* c, int64_t n, const double* zmax, const double
       e[1] = fma(-0.5, e[2], e[1]);
       for (int k = 0; k < N; ++k) {
         const double* K = wk->K + 3 * k;
-        const double u = -fma(K[0], e[0], fma(K[1], e[1], K[2] * e[2])) - wk->kf[k];
-        if (k == 0) v0 = u;
-        const double z = fma(c->pi, u, fma(c->gp, e[2], e[0] + e[1]));
+        // z = −Kη − kf; η⁺ = Āη + e2 v, v = (z − c̄ᵀη)/π, and c̄ᵀη = η0⁺ + π η2 (γ' − 1 = π)
+        const double z = -fma(K[0], e[0], fma(K[1], e[1], K[2] * e[2])) - wk->kf[k];
         const double s12 = e[1] + e[2];
-        e[0] = e[0] + s12;
+        const double e0 = e[0] + s12;
+        const double e2n = c->ipi * (z - e0);
+        const double u = e2n - e[2];
+        if (k == 0) v0 = u;
+        e[0] = e0;
         e[1] = s12;
-        e[2] = e[2] + u;
-        const double r = (wk->hi[k] + wk->lo[k]) / 2;
-        wk->w[k] = (wk->f[k] == 0) ? z - r : u;
+        e[2] = e2n;
+        wk->w[k] = u;
         wk->nf[k] = (z > wk->hi[k] + tol) ? 1 : ((z < wk->lo[k] - tol) ? 2 : 0);
       }
-      // costate from λ_N = ∇V_N = 0: λ_k = c̄ e_k + Āᵀλ_{k+1}, e_k = z_k − r_k + ν_k
+      // costate from λ_N = ∇V_N = 0: λ_k = Fᵀλ_{k+1} − επ v_k c̄; a pinned slot's multiplier
+      // from stationarity in z_k: ν = −((z − r) + επ v + λ2_{k+1}/π), z − r = ±half-width
       double l0 = 0, l1 = 0, l2 = 0;
       int changed = 0;
       for (int k = N - 1; k >= 0; --k) {
         const int f = wk->f[k];
         const double hi = wk->hi[k], lo = wk->lo[k];
-        // pinned: π e + ρ v + λ2_{k+1} = 0 (stationarity in v_k)
-        const double ee = (f == 0) ? wk->w[k] : -fma(c->rho, wk->w[k], l2) * c->ipi;
+        const double ev = c->epi * wk->w[k];
         int nf;
         if (f == 0) {
           nf = wk->nf[k];
         } else {
-          const double r = (hi + lo) / 2;
-          const double t = (f == 1) ? hi : lo;
-          const double nu = ee - (t - r);
+          const double zr = (f == 1) ? (hi - lo) / 2 : -((hi - lo) / 2);
+          const double nu = -(zr + fma(c->ipi, l2, ev));
           const int rel = (f == 1 && nu < -c->tolnu) || (f == 2 && nu > c->tolnu);
           nf = rel ? 0 : f;
         }
         changed |= nf != f;
         wk->nf[k] = (unsigned char)nf;
-        const double s01 = l0 + l1;
-        const double s012 = s01 + l2;
-        l0 = ee + l0;
-        l1 = ee + s01;
-        l2 = fma(c->gp, ee, s012);
+        const double al2 = c->ipi * l2;
+        const double m0 = l0 - al2, m1 = (l0 + l1) - al2;
+        l0 = m0 - ev;
+        l1 = m1 - ev;
+        l2 = fma(-c->gp, ev, m1);
       }
       memcpy(wk->f, wk->nf, (size_t)N);
       if (changed && it >= LQ_MAXIT) {

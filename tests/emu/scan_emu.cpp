@@ -4,6 +4,10 @@
 // kick step (−1: none).  Test infrastructure only.
 #include "hip/hip_runtime.h"
 
+#ifndef EMU_STACK_SHIFT  // log2 of each lane's coroutine stack (the sanitizer build: smaller)
+#define EMU_STACK_SHIFT 20
+#endif
+
 EmuDim3 threadIdx, blockIdx;
 uint64_t emu_buf[64];
 static ucontext_t g_main, g_lane[64];
@@ -66,25 +70,7 @@ int main(int argc, char** argv) {
   emu::ScanArgs& a = g_args;
   // the constants as strict_scan.hip's fill() forms them from a plan
   a.N = N;
-  a.T = T;
-  a.T2 = T * T / 2;
-  a.T3 = T * T * T / 6;
-  a.Tsq = T * T;
-  a.Tcu = a.Tsq * T;
-  const double hgt = hg / a.Tsq;
-  a.pi = 1.0 / 6.0 - hgt;
-  a.ipi = 1.0 / a.pi;
-  a.gp = 7.0 / 6.0 - hgt;
-  a.gp2 = a.gp * a.gp;
-  a.gipi = a.gp / a.pi;
-  a.pig = a.pi * a.gp;
-  a.rho = R / (Q * a.Tcu * a.Tcu);
-  a.quu0 = a.pi * a.pi + a.rho;
-  a.tolnu = 1e-13 / Q;
-  a.iR = 1.0 / a.quu0;
-  a.piR = a.pi / a.quu0;
-  a.rhoR = a.rho / a.quu0;
-  a.rhoP2 = a.rho / (a.pi * a.pi);
+  emu::fill_consts(a, T, T * T / 2, T * T * T / 6, hg, Q, R);
   a.window_mode = 0;
   a.toff = 1;
   a.n = n;
@@ -100,14 +86,14 @@ int main(int argc, char** argv) {
   int32_t status = 0;
   a.status = &status;
   a.cnt = nullptr;
-  std::vector<char> stacks((size_t)64 << 20);
+  std::vector<char> stacks((size_t)64 << EMU_STACK_SHIFT);
   const unsigned waves = g_L == 64 ? 2 : 1;  // the walk's two (walk, axis) instances
   for (unsigned w = 0; w < waves; ++w) {
     blockIdx.x = w;
     for (int l = 0; l < 64; ++l) {
       getcontext(&g_lane[l]);
-      g_lane[l].uc_stack.ss_sp = stacks.data() + ((size_t)l << 20);
-      g_lane[l].uc_stack.ss_size = (size_t)1 << 20;
+      g_lane[l].uc_stack.ss_sp = stacks.data() + ((size_t)l << EMU_STACK_SHIFT);
+      g_lane[l].uc_stack.ss_size = (size_t)1 << EMU_STACK_SHIFT;
       g_lane[l].uc_link = &g_main;
       g_done[l] = false;
       makecontext(&g_lane[l], lane_main, 0);

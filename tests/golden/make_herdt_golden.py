@@ -187,5 +187,87 @@ def main():
     print("saved", os.path.join(HERE, "herdt_default.npz"))
 
 
+# (alpha, beta, gamma) points beyond the class defaults (1e-6, 1, 1): the Herdt QP weights the
+# jerk, the velocity tracking and the ZMP centring by them (zmp_controller.py:740-760,
+# config.py:43-45).
+WEIGHT_POINTS = (
+    (1e-4, 1.0, 1.0),
+    (1e-6, 10.0, 0.1),
+    (1e-8, 0.1, 10.0),
+    (1e-5, 1.0, 100.0),
+)
+
+
+def main_weights():
+    """Non-default Herdt weights → herdt_weights.npz: per point w the default walk's rollout
+    (com, y_hist, foot_hist; v_ref and states are the ones of herdt_default.npz) and 6 single
+    steps (inputs + the exact solution), every QP captured from the reference's own code."""
+    sys.modules["cvxpy"] = make_cp()
+    os.environ["PYTHONDONTWRITEBYTECODE"] = "1"
+    sys.dont_write_bytecode = True
+    sys.path.insert(0, "/root/reference")
+    from src.mpc_bipedal.config import MPCConfig
+    from src.mpc_bipedal.controllers import ZMPController
+    from src.mpc_bipedal.generators.speed_generation import SpeedTrajectoryGenerator
+    from src.mpc_bipedal.generators.cop_generator import State
+
+    SMAP = {State.STANDING: HO.STANDING, State.DOUBLE_SUPPORT: HO.DOUBLE_SUPPORT,
+            State.SINGLE_SUPPORT: HO.SINGLE_SUPPORT}
+    out = {"weights": np.array(WEIGHT_POINTS)}
+    worst = dict(stationarity=0.0, primal=0.0, dual=0.0, complementarity=0.0)
+    for w, (al, be, ga) in enumerate(WEIGHT_POINTS):
+        cfg = MPCConfig(method="herdt", add_force=True, alpha=al, beta=be, gamma=ga)
+        CAPTURE["N"], CAPTURE["qps"] = cfg.horizon, []
+        sg = SpeedTrajectoryGenerator(cfg)
+        vx, vy, states = sg.generate_speed_and_state(save_footsteps=False)
+        v_ref = np.stack([vx, vy], 1)
+        st_int = np.array([SMAP[s] for s in states], np.int8)
+        ctl = ZMPController(cfg)
+        ctl.plot_solution = lambda *a, **k: None
+        calls = []
+        orig = ctl.predict_herdt_joint
+
+        def record(*args):
+            calls.append([np.array(a, copy=True) if isinstance(a, np.ndarray) else a
+                          for a in args])
+            return orig(*args)
+        ctl.predict_herdt_joint = record
+        com, y_hist, foot = ctl.generate_com_trajectory(np.zeros((3, 1)), np.zeros((3, 1)),
+                                                        v_ref=v_ref, state_ref=np.array(states))
+        qps = CAPTURE["qps"]
+        for k in worst:
+            worst[k] = max(worst[k], max(q["kkt"].get(k, 0.0) for q in qps))
+        com2, yh2, foot2, _ = HO.herdt_rollout(cfg, np.zeros(3), np.zeros(3), v_ref, st_int)
+        e = max(np.abs(com2 - com).max(), np.abs(foot2 - foot).max())
+        print(f"w{w} (alpha={al:g}, beta={be:g}, gamma={ga:g}): {len(qps)} QPs, oracle rollout "
+              f"vs reference-driven {e:.2e}", flush=True)
+        assert e <= 1e-12
+        out[f"w{w}_v_ref"], out[f"w{w}_states"] = v_ref, st_int
+        out[f"w{w}_com"], out[f"w{w}_y_hist"], out[f"w{w}_foot_hist"] = com, y_hist[:, :, 0], foot
+        n = len(v_ref)
+        pick = np.linspace(0, n - 2, 6).astype(int).tolist()
+        for j, i in enumerate(pick):
+            (x_in, y_in, vwin, xfc, yfc, cur, swin, nbs, _nbn, _xa, _ya, side, _idx) = calls[i]
+            Q, p, G, h, N, m = HO.herdt_qp(cfg, x_in, y_in, vwin, float(xfc), float(yfc),
+                                           SMAP[cur], np.array([SMAP[t] for t in swin], np.int8),
+                                           side)
+            assert Q.shape == qps[i]["Q"].shape
+            s = dict(x=np.asarray(x_in).ravel(), y=np.asarray(y_in).ravel(), v=vwin,
+                     fx=float(xfc), fy=float(yfc), cur=SMAP[cur],
+                     win=np.array([SMAP[t] for t in swin], np.int8),
+                     side=0 if side == "left" else 1, sol=qps[i]["x"], N=N, m=m)
+            for key, val in s.items():
+                out[f"w{w}_step{j}_{key}"] = np.asarray(val)
+        out[f"w{w}_n_steps_saved"] = len(pick)
+    print(f"worst KKT {worst}")
+    out["kkt_worst"] = np.array([worst[k] for k in ("stationarity", "primal", "dual",
+                                                     "complementarity")])
+    np.savez_compressed(os.path.join(HERE, "herdt_weights.npz"), **out)
+    print("saved", os.path.join(HERE, "herdt_weights.npz"))
+
+
 if __name__ == "__main__":
-    main()
+    if "--weights" in sys.argv:
+        main_weights()
+    else:
+        main()

@@ -372,8 +372,109 @@ def main_long():
     print("saved", os.path.join(HERE, "strict_long_ref.npz"))
 
 
+# (Q, R, h, g) points beyond default.json's (Q = 1, R = 1e-6, h = 0.75, g = 9.81): the strict
+# QP depends on all four (zmp_controller.py:174,184-188; config.py:31-35).  R/Q spans 1e-10 ..
+# 1e-2, Q 0.1 .. 100, h 0.5 .. 1.0, g 3.71 .. 9.81.
+WEIGHT_POINTS = (
+    (1.0, 1e-9, 0.75, 9.81),
+    (100.0, 1e-2, 1.0, 9.81),
+    (0.1, 1e-3, 0.5, 9.81),
+    (10.0, 1e-5, 0.9, 3.71),
+    (0.1, 1e-11, 1.0, 9.81),
+)
+
+
+def main_weights():
+    """Non-default weights → strict_weights_ref.npz.  Per point w (WEIGHT_POINTS[w]):
+    * w{w}_n{64,150}_com / _yhist: the default.json walk at that horizon (the reference's own
+      CoPGenerator), generate_com_trajectory(strict=True) with a 400 N kick at n//2, from rest;
+    * w{w}_step{16,64,150}_x / _zmax / _zmin / _out: 48 cold predict_wieber_axis calls with
+      heavily active bounds (as main()'s step cases)."""
+    sys.modules["cvxpy"] = make_cp()
+    sys.dont_write_bytecode = True
+    sys.path.insert(0, REF)
+    from src.mpc_bipedal.config import MPCConfig
+    from src.mpc_bipedal.generators import CoPGenerator
+    from src.mpc_bipedal.controllers import ZMPController
+
+    def instrument(ctl):
+        orig = ctl.predict_wieber_axis
+
+        def record(x_init, nb_steps, z_max, z_min):
+            _Rec.call = (np.array(x_init, np.float64), nb_steps, np.array(z_max), np.array(z_min),
+                         ctl.config)
+            out = orig(x_init, nb_steps, z_max, z_min)
+            _Rec.axis ^= 1
+            return out
+        ctl.predict_wieber_axis = record
+        return ctl
+
+    out = {"weights": np.array(WEIGHT_POINTS)}
+    dev = 0.0
+    rng = np.random.default_rng(20251228)
+    for w, (Qv, Rv, hv, gv) in enumerate(WEIGHT_POINTS):
+        for N in (64, 150):
+            d = default_mpc_dict()
+            d.update(horizon=N, strict=True, add_force=True, F_ext=400.0, Q=Qv, R=Rv, h=hv,
+                     g=gv)
+            cfg = MPCConfig(**d)
+            zmax, zmin, _ = CoPGenerator(cfg).generate_cop_trajectory(save_footsteps=False)
+            n = len(zmax)
+            ctl = instrument(ZMPController(cfg))
+            _Rec.rollout, _Rec.axis, _Rec.warm = True, 0, [None, None]
+            with contextlib.redirect_stdout(io.StringIO()), \
+                    contextlib.redirect_stderr(io.StringIO()):
+                com, y_hist = ctl.generate_com_trajectory(np.zeros((3, 1)), np.zeros((3, 1)),
+                                                          zmax, zmin)
+            out[f"w{w}_n{N}_zmax"], out[f"w{w}_n{N}_zmin"] = zmax, zmin
+            out[f"w{w}_n{N}_com"], out[f"w{w}_n{N}_yhist"] = com, y_hist[:, :, 0]
+            ref = O.rollout_strict(np.zeros(3), np.zeros(3), zmax, zmin, N, cfg.dt, hv, gv, Qv,
+                                   Rv, kick=cfg.dt * cfg.F_ext / cfg.m, kick_step=n // 2)
+            e = max(float(np.abs(ref[:, :, 0] - com).max()),
+                    float(np.abs(ref[:, 1] - y_hist[:, :, 0]).max()))
+            dev = max(dev, e)
+            print(f"w{w} (Q={Qv:g}, R={Rv:g}, h={hv:g}, g={gv:g}) N={N}: rollout vs oracle "
+                  f"max |d| {e:.2e}, {_Rec.n_qp} QPs, max rel problem diff {_Rec.max_rel:.2e}",
+                  flush=True)
+        _Rec.rollout = False
+        for N in (16, 64, 150):
+            d = default_mpc_dict()
+            d.update(horizon=N, strict=True, Q=Qv, R=Rv, h=hv, g=gv)
+            ctl = instrument(ZMPController(MPCConfig(**d)))
+            B = 48
+            x = np.stack([rng.uniform(-0.05, 0.05, B), rng.uniform(-0.6, 0.6, B),
+                          rng.uniform(-6, 6, B)], 1)
+            ctr = rng.uniform(-0.05, 0.05, (B, 1)) + np.cumsum(rng.normal(0, 0.003, (B, N)), 1)
+            zmax_w = ctr + rng.uniform(0.005, 0.06, (B, N))
+            zmin_w = ctr - rng.uniform(0.005, 0.06, (B, N))
+            res = np.stack([ctl.predict_wieber_axis(x[b].reshape(3, 1), N,
+                                                    zmax_w[b].reshape(N, 1),
+                                                    zmin_w[b].reshape(N, 1)).ravel()
+                            for b in range(B)])
+            ref = O.strict_step_batch(x, zmax_w, zmin_w, N, 1.5 / N, hv, gv, Qv, Rv)
+            e = float(np.abs(res - ref).max())
+            dev = max(dev, e)
+            out[f"w{w}_step{N}_x"], out[f"w{w}_step{N}_zmax"] = x, zmax_w
+            out[f"w{w}_step{N}_zmin"], out[f"w{w}_step{N}_out"] = zmin_w, res
+            print(f"w{w} step N={N}: {B} cold calls, vs oracle max |d| {e:.2e}", flush=True)
+    print(f"{_Rec.n_qp} captured QPs; max rel problem diff {_Rec.max_rel:.2e}; KKT {_Rec.kkt}")
+    assert _Rec.max_rel <= 1e-13, _Rec.max_rel
+    assert _Rec.kkt["primal"] <= 1e-13 and _Rec.kkt["stationarity"] <= 1e-10, _Rec.kkt
+    assert _Rec.kkt["dual_hi"] <= 1e-10 and _Rec.kkt["dual_lo"] <= 1e-10, _Rec.kkt
+    assert dev <= 1e-12, dev
+    out["max_rel_problem_diff"] = _Rec.max_rel
+    out["kkt_worst"] = np.array([_Rec.kkt[k] for k in ("primal", "stationarity", "dual_hi",
+                                                         "dual_lo")])
+    out["max_abs_vs_oracle"] = dev
+    out["n_qps"] = _Rec.n_qp
+    np.savez_compressed(os.path.join(HERE, "strict_weights_ref.npz"), **out)
+    print("saved", os.path.join(HERE, "strict_weights_ref.npz"))
+
+
 if __name__ == "__main__":
     if "--long" in sys.argv:
         main_long()
+    elif "--weights" in sys.argv:
+        main_weights()
     else:
         main()

@@ -887,6 +887,56 @@ def test_strict_solvers_vs_reference(solver):
             plan(600, strict=True).set_option("strict_solver", solver)
 
 
+@pytest.mark.parametrize("solver", (3, 4))
+@pytest.mark.parametrize("w", range(5))
+def test_strict_weights_vs_reference(w, solver):
+    """Strict parity beyond default.json's weights (the QP depends on Q, R, h and g:
+    zmp_controller.py:174,184-188, config.py:31-35).  tests/golden/strict_weights_ref.npz holds,
+    per (Q, R, h, g) point — R/Q from 1e-10 to 1e-2, Q 0.1 .. 100, h 0.5 .. 1.0, g 3.71 and
+    9.81 — the reference's own strict branch (recording cvxpy stand-in, exact answers,
+    make_strict_ref_golden.py --weights) on the default.json walk at N = 64 and 150 with a
+    400 N kick, and 48 cold heavily-active predict_wieber_axis calls at N = 16, 64, 150.  The
+    LQ kernel (3) and the parallel-in-time kernel (4): CoM and ZMP RMSE ≤ 1e-9, single solves
+    ≤ 1e-9 relative, every status 0."""
+    d = golden("strict_weights_ref.npz")
+    Qv, Rv, hv, gv = (float(v) for v in d["weights"][w])
+    cz = np.array([1.0, 0.0, -hv / gv])
+    for N in (64, 150):
+        zx, zn = d[f"w{w}_n{N}_zmax"], d[f"w{w}_n{N}_zmin"]
+        n, dt = len(zx), 1.5 / N
+        p = Plan(torch.cuda.current_device(), N, dt, hv, gv, Qv, Rv, True)
+        p.set_option("strict_solver", solver)
+        h, st = p.rollout(zx, zn, np.zeros((1, 2, 3)), kick=np.array([dt * 400.0 / M]),
+                          kick_step=n // 2)
+        assert int(st.abs().max()) == 0
+        h = h.cpu().numpy()[0]
+        assert rmse(h[:, :, 0], d[f"w{w}_n{N}_com"]) <= 1e-9, N
+        assert rmse(h[:, 1] @ cz, d[f"w{w}_n{N}_yhist"] @ cz) <= 1e-9, N
+        assert np.abs(h[:, 1] - d[f"w{w}_n{N}_yhist"]).max() <= 1e-6, N
+    for N in (16, 64, 150):
+        p = Plan(torch.cuda.current_device(), N, 1.5 / N, hv, gv, Qv, Rv, True)
+        p.set_option("strict_solver", solver)
+        out, st = p.step(d[f"w{w}_step{N}_x"], d[f"w{w}_step{N}_zmax"], d[f"w{w}_step{N}_zmin"])
+        ref = d[f"w{w}_step{N}_out"]
+        assert int(st.abs().max()) == 0
+        assert np.abs(out.cpu().numpy() - ref).max() <= 1e-9 * max(1.0, np.abs(ref).max()), N
+
+
+@pytest.mark.parametrize("w", (0, 2))
+def test_strict_weights_drop_in(w):
+    """The drop-in at non-default weights: ZMPController(MPCConfig(Q, R, h, g, strict=True))
+    .generate_com_trajectory on the default walk equals the reference-driven strict rollout
+    (strict_weights_ref.npz) at ≤ 1e-9 CoM RMSE."""
+    d = golden("strict_weights_ref.npz")
+    Qv, Rv, hv, gv = (float(v) for v in d["weights"][w])
+    c = ZMPController(MPCConfig(horizon=150, strict=True, add_force=True, F_ext=400.0, Q=Qv,
+                                R=Rv, h=hv, g=gv))
+    com, y_hist = c.generate_com_trajectory(np.zeros((3, 1)), np.zeros((3, 1)),
+                                            d[f"w{w}_n150_zmax"], d[f"w{w}_n150_zmin"])
+    assert rmse(com, d[f"w{w}_n150_com"]) <= 1e-9
+    assert rmse(y_hist[:, :, 0] @ c.C, d[f"w{w}_n150_yhist"] @ c.C) <= 1e-9
+
+
 @pytest.mark.parametrize("B,auto", ((2, 4), (300, 4), (2100, 4), (12300, 3)))
 def test_strict_small_and_large_batch_paths_agree(B, auto):
     """The automatic choice (ZMPC_OPT_STRICT_SOLVER = 0) takes the parallel-in-time kernel up to
