@@ -207,44 +207,82 @@ def herdt_bench(args, rank, world, dev, dist_on):
         "cpu_baseline": cpu, "com_rmse_vs_ref": com_rmse_ref}
 
 
-def _herdt_cpu_baseline(cfg, v_ref, st, hist_gpu, foot_gpu, x0_h, kick_h, budget_s):
-    """CPU leg for config 6 (rank 0): the oracle's exact Herdt rollout (herdt_oracle; the
-    reference's cvxpy/OSQP is not installed) on walk 0, timed for budget_s of CPU work (a
-    prefix of the walk), 1 process at the default BLAS threads; parity of the GPU walk 0."""
+def _herdt_port_qps(cfg, vpad, spad, hist_w, foot_w, kick, i0, budget_s):
+    """The oracle's exact Herdt step (herdt_oracle.herdt_step, the reference's
+    predict_herdt_joint restated; its cvxpy/OSQP is not installed) over consecutive timesteps
+    of one GPU walk from timestep i0, each QP fed the GPU walk's own state and foot and checked
+    against the GPU's next state, until budget_s: (QPs, seconds, max |Δstate|)."""
     from oracle import herdt_oracle as HO
-    n = len(st)
+    n = hist_w.shape[0]
     N = cfg.horizon
-    vpad = np.vstack([v_ref, np.repeat(v_ref[-1:], N, axis=0)])
-    spad = np.concatenate([st, np.repeat(st[-1:], N)])
-    x, y = x0_h[0, 0].copy(), x0_h[0, 1].copy()
-    fx, fy = 0.0, float(cfg.foot_spread)
-    cur = spad[0]
+    # the support side at i0: flips after every single-support phase (zmp_controller.py:497-529)
     side = "left"
+    for i in range(i0):
+        if spad[i + 1] != spad[i] and spad[i] == 2:
+            side = "left" if side == "right" else "right"
+    cur = spad[i0]
     t0 = time.perf_counter()
     steps, err = 0, 0.0
-    for i in range(n - 1):
+    for i in range(i0, n - 1):
         if time.perf_counter() - t0 > budget_s and steps >= 2:
             break
-        # the GPU walk's own state and foot as input: each timed QP is checked one by one
-        x, y = hist_gpu[0, i, 0], hist_gpu[0, i, 1]
-        fx, fy = foot_gpu[0, i]
+        x, y = hist_w[i, 0], hist_w[i, 1]
+        fx, fy = foot_w[i]
         xn, yn, _, _ = HO.herdt_step(cfg, x, y, vpad[i + 1: i + 1 + N], fx, fy, cur,
                                      spad[i + 1: i + 1 + N], side)
         if i == n // 2:
-            yn = yn - np.array([0.0, kick_h[0], 0.0])
-        err = max(err, float(np.abs(xn - hist_gpu[0, i + 1, 0]).max()),
-                  float(np.abs(yn - hist_gpu[0, i + 1, 1]).max()))
+            yn = yn - np.array([0.0, kick, 0.0])
+        err = max(err, float(np.abs(xn - hist_w[i + 1, 0]).max()),
+                  float(np.abs(yn - hist_w[i + 1, 1]).max()))
         if spad[i + 1] != cur and cur == 2:
             side = "left" if side == "right" else "right"
         if spad[i + 1] != cur:
             cur = spad[i + 1]
         steps += 1
-    el = time.perf_counter() - t0
-    return {"value": steps / el, "unit": "QP solves/s", "cores": cpu_share(), "kind": "port",
-            "sample": f"{steps} consecutive joint QPs of walk 0 (exact Goldfarb-Idnani NumPy "
-                      "port of predict_herdt_joint; the reference's cvxpy/OSQP is not "
-                      "installed), default BLAS threads",
-            "seconds": el, "max_abs_state_gpu_vs_port": err}
+    return steps, time.perf_counter() - t0, err
+
+
+def _herdt_port_worker(job):
+    """One process of the multi-process Herdt CPU leg (spawned; numpy only, 1 BLAS thread)."""
+    from threadpoolctl import threadpool_limits
+    with threadpool_limits(1):
+        return _herdt_port_qps(*job)
+
+
+def _herdt_cpu_baseline(cfg, v_ref, st, hist_gpu, foot_gpu, x0_h, kick_h, budget_s):
+    """CPU leg for config 6 (rank 0), §8d(ii): P processes x 1 BLAS thread (P = this process's
+    CPU share), process p on GPU walk p from a timestep spread over the walk (so the sample
+    covers standing, double and single support and every footstep count), each timing the
+    oracle's exact joint QP for budget_s; the sum of their rates.  Also one process at the
+    default BLAS threads on walk 0 (§8d(i)).  Parity: every timed QP against the GPU walk."""
+    n = len(st)
+    N = cfg.horizon
+    vpad = np.vstack([v_ref, np.repeat(v_ref[-1:], N, axis=0)])
+    spad = np.concatenate([st, np.repeat(st[-1:], N)])
+    P = cpu_share()
+    W = min(P, hist_gpu.shape[0])
+    jobs = [(cfg, vpad, spad, hist_gpu[w], foot_gpu[w], float(kick_h[w]),
+             int((n - 2) * w / max(1, W)), budget_s) for w in range(W)]
+    import multiprocessing
+    from concurrent.futures import ProcessPoolExecutor
+    with ProcessPoolExecutor(max_workers=W,
+                             mp_context=multiprocessing.get_context("spawn")) as ex:
+        res = list(ex.map(_herdt_port_worker, jobs))
+    qps = sum(r[0] for r in res)
+    multi = {"value": sum(r[0] / r[1] for r in res if r[1] > 0), "unit": "QP solves/s",
+             "cores": W, "kind": "port",
+             "sample": f"{W} processes x 1 BLAS thread, {qps} joint QPs (process p: walk p from "
+                       "timestep p(n-2)/P, exact Goldfarb-Idnani NumPy port of "
+                       "predict_herdt_joint; the reference's cvxpy/OSQP is not installed), "
+                       f"≈{budget_s:.0f} s each",
+             "max_abs_state_gpu_vs_port": max(r[2] for r in res)}
+    s_steps, s_el, s_err = _herdt_port_qps(cfg, vpad, spad, hist_gpu[0], foot_gpu[0],
+                                           float(kick_h[0]), 0, budget_s)
+    multi["single_process_default_blas"] = {
+        "value": s_steps / s_el, "unit": "QP solves/s", "cores": P, "kind": "port",
+        "sample": f"{s_steps} consecutive joint QPs of walk 0, 1 process at the default BLAS "
+                  "threads", "seconds": s_el, "max_abs_state_gpu_vs_port": s_err}
+    return multi
 
 
 def plan_record(plan):

@@ -57,6 +57,11 @@ namespace {
 using namespace zmpc_eta;
 
 constexpr int LQ_MAXIT = 64;  // active-set pass cap (as strict.hip)
+#ifdef ZMPC_DIAG
+constexpr bool kLqProf = true;  // per-phase clocks (ZMPC_LQ_PROF), diagnostics build only
+#else
+constexpr bool kLqProf = false;
+#endif
 #ifndef ZMPC_LQ_S  // (A/B builds only: make ab)
 #define ZMPC_LQ_S 8
 #endif
@@ -114,6 +119,7 @@ struct LqArgs {
   int* queue;
   int64_t qblock0;       // first block not in the grid
   int64_t nblocks;       // blocks of the whole launch (G waves each)
+  unsigned long long* prof;  // diagnostics build only (ZMPC_LQ_PROF): clocks per phase and axis
 };
 
 template <int S>
@@ -126,7 +132,6 @@ template <int S>
 struct SegOut {  // a segment's feedback (v = −K η − kff) and forward outputs, per step
   double K0[S], K1[S], K2[S], kf[S];
   double w[S];  // forward: v_k (= T³u_k)
-  int nf[S];    // forward: the free slots' primal verdict (0 stays free, ±1 violated)
 };
 
 // A free-tail step: P, K, Qux and 1/Quu come from the table, only s moves (strict_eta.h's
@@ -334,10 +339,12 @@ __device__ __forceinline__ void seg_tail(const LqArgs& a, const double* __restri
 }
 
 // Forward through segment j: roll the trajectory out (η advances to the segment's end), primal
-// check of the free slots, and the per-step input of the costate sweep.
+// check of the free slots — their new flags go to LDS here (predicated stores; the pinned
+// slots' come from the costate) — and the per-step input of the costate sweep.
 template <int S, bool FULL>
 __device__ __forceinline__ void seg_forward(const LqArgs& a, int j, const SegIn<S>& in,
-                                            SegOut<S>& g, double* x, double& u0) {
+                                            SegOut<S>& g, double* x, double& u0, bool& changed,
+                                            int& kl, const Flags& fl, int lane) {
   const double tol = 1e-13;  // as strict.hip (tolz)
 #pragma unroll
   for (int q = 0; q < S; ++q) {
@@ -348,7 +355,12 @@ __device__ __forceinline__ void seg_forward(const LqArgs& a, int j, const SegIn<
       if (k == 0) u0 = u;
       const double d = z - in.r[q], ht = in.h[q] + tol;
       g.w[q] = u;
-      g.nf[q] = (d > ht) ? 1 : ((d < -ht) ? -1 : 0);
+      const int nf = (d > ht) ? 1 : ((d < -ht) ? -1 : 0);
+      if (in.f[q] == 0) {
+        fl.set(k, lane, nf);
+        changed |= nf != 0;
+        kl = nf ? k : kl;  // (slots ascend)
+      }
     }
   }
 }
@@ -379,8 +391,8 @@ __device__ __forceinline__ void seg_forward_tail(const LqArgs& a, const double* 
 }
 
 // Costate sweep back through segment j from λ at its end (λ_k = ∇V_k(η_k) = Fᵀλ_{k+1} − επ v_k c̄,
-// strict_eta.h): the bound multipliers ν_k of the pinned slots, dual check, the slot's new flag;
-// kl = the last slot pinned in the new set.
+// strict_eta.h): the bound multipliers ν_k of the pinned slots, dual check, the pinned slots'
+// new flags (the free slots' were set by the forward); kl = the last slot pinned in the new set.
 template <int S, bool FULL>
 __device__ __forceinline__ void seg_costate(const LqArgs& a, int j, const SegIn<S>& in,
                                             const SegOut<S>& g, double* lam, bool& changed,
@@ -393,13 +405,13 @@ __device__ __forceinline__ void seg_costate(const LqArgs& a, int j, const SegIn<
       {
         const double sg = (double)f;
         const double nu = pinned_nu(a, sg, in.h[q], g.w[q], lam);  // ν / Q (pinned slots only)
-        // wrong-signed multiplier (ν < 0 at z_max, ν > 0 at z_min): σν < −tol; free: 0 < −tol
+        // wrong-signed multiplier (ν < 0 at z_max, ν > 0 at z_min): σν < −tol
         const bool rel = sg * nu < -a.tolnu;
-        // the slot's new flag, written unconditionally (branch-free)
-        const int nf = (f == 0) ? g.nf[q] : (rel ? 0 : f);
-        fl.set(k, lane, nf);
-        changed |= nf != f;
-        kl = (nf != 0 && k > kl) ? k : kl;
+        if (f != 0) {
+          fl.set(k, lane, rel ? 0 : f);
+          changed |= rel;
+          kl = (!rel && k > kl) ? k : kl;
+        }
       }
       costate_step(a, g.w[q], lam);
     }
@@ -407,18 +419,22 @@ __device__ __forceinline__ void seg_costate(const LqArgs& a, int j, const SegIn<
 }
 
 // Sweep B through one working-set segment: Riccati from its checkpoint, forward, costate.
-template <int S, bool FULL>
+// (lap: the diagnostics build's phase clock)
+template <int S, bool FULL, class Lap>
 __device__ __forceinline__ void seg_sweep_b(const LqArgs& a, int j, Ric& v, const SegIn<S>& in,
                                             SegOut<S>& g, double* xs, double& u0, bool& changed,
-                                            int& kl, const Flags& fl, int lane) {
+                                            int& kl, const Flags& fl, int lane, Lap& lap) {
   const Ric ve = v;  // V at the segment's end
   seg_riccati<S, FULL, true, false>(a, j, v, in, g);
-  seg_forward<S, FULL>(a, j, in, g, xs, u0);
+  lap(4);
+  seg_forward<S, FULL>(a, j, in, g, xs, u0, changed, kl, fl, lane);
+  lap(5);
   double lam[3];
   lam[0] = fma(ve.p00, xs[0], fma(ve.p01, xs[1], ve.p02 * xs[2])) - ve.s0;
   lam[1] = fma(ve.p01, xs[0], fma(ve.p11, xs[1], ve.p12 * xs[2])) - ve.s1;
   lam[2] = fma(ve.p02, xs[0], fma(ve.p12, xs[1], ve.p22 * xs[2])) - ve.s2;
   seg_costate<S, FULL>(a, j, in, g, lam, changed, kl, fl, lane);
+  lap(6);
 }
 
 // Checkpoints are written once and read once per pass.  With per-walk bounds (whose rows are
@@ -517,7 +533,9 @@ __global__ void __launch_bounds__(64 * G, 2)
   const Flags fl{reinterpret_cast<signed char*>(lq_smem) + (size_t)wave * fbytes * 64};
   double* ck = a.ck + (size_t)gw * a.NS * kCkStride;
   const CkIO<NT> io{};
-  unsigned long long n_wave_pass = 0, n_lane_pass = 0, n_ws_slots = 0;
+  // (per-lane counts in 32 bits: ≤ 2(n − 1)·64 passes and ·N slots per lane and task group)
+  unsigned long long n_wave_pass = 0;
+  unsigned n_lane_pass = 0, n_ws_slots = 0;
 #ifdef ZMPC_DIAG
   unsigned long long n_sb_ws = 0, n_sb_free = 0;
 #endif
@@ -546,13 +564,18 @@ __global__ void __launch_bounds__(64 * G, 2)
   const int64_t b = (valid && a.perm) ? (int64_t)a.perm[pos] : pos;
   Lane L;
   L.lane = lane;
-  L.col = (int)(pos & 63);
+  L.col = RUNS ? lane : (int)(pos & 63);  // (pos = 64·group + lane; the forms allocate best)
   {
+    // the wave's (axis, group) tables; the run tables' base wave-uniform (SGPRs), the lane's
+    // column added per access
     const int64_t g = a.shared ? 0 : (pos >> 6);
     if constexpr (RUNS) {
       const int64_t off = ((int64_t)axis * a.groups + g) * a.rstride;
-      L.rs = a.rs + off;
-      L.rt = a.rt + off;
+      const int lo = __builtin_amdgcn_readfirstlane((int)(off & 0xffffffff));
+      const int hi = __builtin_amdgcn_readfirstlane((int)(off >> 32));
+      const int64_t uoff = ((int64_t)hi << 32) | (uint32_t)lo;
+      L.rs = a.rs + uoff;
+      L.rt = a.rt + uoff;
     } else {
       L.hl = a.hl + ((int64_t)axis * a.groups + g) * a.rows * 64;
     }
@@ -582,9 +605,9 @@ __global__ void __launch_bounds__(64 * G, 2)
     }
   }
   int fq = 0;
-  const int64_t kstep =
+  const int kstep =
       (!a.window_mode && axis == 1 && a.kick != nullptr && valid)
-          ? (a.kick_steps ? a.kick_steps[b] : a.kick_step)
+          ? (int)(a.kick_steps ? a.kick_steps[b] : a.kick_step)
           : -1;
   const double kv = (kstep >= 0) ? a.kick[b] : 0.0;
 
@@ -596,6 +619,18 @@ __global__ void __launch_bounds__(64 * G, 2)
   bool active = valid && a.nsteps > 0;
   int it = 0;
   int klast = -1;      // last pinned slot of this lane's working set (−1: none)
+  // diagnostics: clocks of sweep A, sweep B's working-set and tail segments, the rest; task
+  // [0] sweep A tail, [1] sweep A working set, [2] sweep B's segment set-up and checkpoint
+  // wait, [4] its Riccati recompute, [5] forward, [6] costate, [7] sweep B tail, [3] the rest
+  unsigned long long pc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long pt = (kLqProf && a.prof) ? clock64() : 0, ptask = pt;
+  auto lap = [&](int ph) {
+    if (kLqProf && a.prof) {
+      const unsigned long long t = clock64();
+      pc[ph] += t - pt;
+      pt = t;
+    }
+  };
   while (__any(active)) {
     ++n_wave_pass;
     int imin = active ? (int)i : 0x7fffffff;
@@ -606,6 +641,7 @@ __global__ void __launch_bounds__(64 * G, 2)
     for (int o = 32; o > 0; o >>= 1) kw = max(kw, __shfl_xor(kw, o));
     const int jt = __builtin_amdgcn_readfirstlane(kw < 0 ? 0 : kw / S + 1);
     if (part) {
+      lap(3);
       ++n_lane_pass;
       n_ws_slots += (unsigned)min(jt * S, N);
       double u0 = 0.0;
@@ -630,6 +666,7 @@ __global__ void __launch_bounds__(64 * G, 2)
           else
             seg_tail<S, false, false>(a, tab, j, v, cur, g);
         }
+        lap(0);
         if (jt < a.NS) {  // V at the tail's first slot: P from the table
           const double* t = tab + (size_t)jt * S * TAB;
           v.p00 = t[4];
@@ -660,6 +697,7 @@ __global__ void __launch_bounds__(64 * G, 2)
               seg_riccati<S, false, false, false>(a, j, v, cur, g);
           }
         }
+        lap(1);
         // sweep B: per segment from the front — recompute its steps from the checkpoint,
         // forward, then (working-set segments) the costate back through it
         double xs[3];  // η
@@ -677,6 +715,10 @@ __global__ void __launch_bounds__(64 * G, 2)
           else
             seg_load<S, true>(a, j, L, i, fl, cur);
           ck_load(io, ck, j, v, lane);
+          if (kLqProf && a.prof) {  // (diagnostics: the checkpoint's arrival timed apart)
+            __builtin_amdgcn_s_waitcnt(0);
+            lap(2);
+          }
 #ifdef ZMPC_DIAG
           ++n_sb_ws;  // diagnostics: sweep-B working-set segments, and those no lane pins
           if (seg_free(cur)) ++n_sb_free;
@@ -686,9 +728,9 @@ __global__ void __launch_bounds__(64 * G, 2)
           // costate — spills at 256 VGPRs: 74.9 vs 65.0 ms, and 66.7 ms at S = 6,
           // profiles/r4/r4n/)
           if (j < jfull) {
-            seg_sweep_b<S, true>(a, j, v, cur, g, xs, u0, changed, kl, fl, lane);
+            seg_sweep_b<S, true>(a, j, v, cur, g, xs, u0, changed, kl, fl, lane, lap);
           } else {
-            seg_sweep_b<S, false>(a, j, v, cur, g, xs, u0, changed, kl, fl, lane);
+            seg_sweep_b<S, false>(a, j, v, cur, g, xs, u0, changed, kl, fl, lane, lap);
           }
         }
 #pragma unroll 1
@@ -706,6 +748,7 @@ __global__ void __launch_bounds__(64 * G, 2)
             seg_forward_tail<S, false>(a, tab, j, cur, g, xs, u0, changed, kl, fl, lane);
           }
         }
+        lap(7);
       }
       ++it;
       if (changed && it >= LQ_MAXIT) {
@@ -720,7 +763,7 @@ __global__ void __launch_bounds__(64 * G, 2)
         xn[0] = x[0] + a.T * x[1] + a.T2 * x[2] + a.T3 * u0;
         xn[1] = x[1] + a.T * x[2] + a.T2 * u0;
         xn[2] = x[2] + a.T * u0;
-        if (i == kstep) xn[1] -= kv;  // force kick (zmp_controller.py:90,105-106)
+        if ((int)i == kstep) xn[1] -= kv;  // force kick (zmp_controller.py:90,105-106)
         if (!(isfinite(xn[0]) && isfinite(xn[1]) && isfinite(xn[2]))) fq |= ZMPC_ST_NONFINITE;
         x[0] = xn[0];
         x[1] = xn[1];
@@ -756,6 +799,15 @@ __global__ void __launch_bounds__(64 * G, 2)
       }
     }
   }
+  if (kLqProf && a.prof) {
+    lap(3);
+    pc[8] = clock64() - ptask;
+    if (lane == 0) {
+#pragma unroll
+      for (int q = 0; q < 9; ++q) atomicAdd(a.prof + axis * 10 + q, pc[q]);
+      atomicAdd(a.prof + axis * 10 + 9, 1ull);
+    }
+  }
   if (valid && a.status != nullptr) {
     if (a.window_mode)
       a.status[b] = fq;
@@ -783,15 +835,16 @@ __global__ void __launch_bounds__(64 * G, 2)
     run_task(gw);  // one task per wave (the host takes the queue form for 8-wave blocks only)
   }
   if (a.cnt) {
+    unsigned long long lp = n_lane_pass, ws = n_ws_slots;
     for (int o = 32; o > 0; o >>= 1) {
-      n_lane_pass += __shfl_xor(n_lane_pass, o);
-      n_ws_slots += __shfl_xor(n_ws_slots, o);
+      lp += __shfl_xor(lp, o);
+      ws += __shfl_xor(ws, o);
       itmax = max(itmax, (unsigned)__shfl_xor((int)itmax, o));
     }
     if (lane == 0) {
       atomicAdd(a.cnt + 0, n_wave_pass);
-      atomicAdd(a.cnt + 1, n_lane_pass);
-      atomicAdd(a.cnt + 2, n_ws_slots);
+      atomicAdd(a.cnt + 1, lp);
+      atomicAdd(a.cnt + 2, ws);
       if (gw == 0) atomicAdd(a.cnt + 3, 1ull);
 #ifdef ZMPC_DIAG  // (the Herdt counter slots [6], [7], unused by a strict launch)
       atomicAdd(a.cnt + 6, n_sb_ws);
@@ -1016,9 +1069,36 @@ hipError_t launch_lq(const zmpc_plan* p, LqArgs& a, int64_t waves, hipStream_t s
       a.nblocks = blocks;
     }
   }
+#ifdef ZMPC_DIAG
+  static unsigned long long* prof = [] {  // diagnostics build: per-phase clocks to stderr
+    unsigned long long* q = nullptr;
+    if (getenv("ZMPC_LQ_PROF") && hipMalloc((void**)&q, 20 * sizeof(unsigned long long)) != hipSuccess)
+      q = nullptr;
+    return q;
+  }();
+  if (prof) (void)hipMemsetAsync(prof, 0, 20 * sizeof(unsigned long long), s);
+  a.prof = prof;
+#else
+  a.prof = nullptr;
+#endif
   hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(64 * var->G), lds, s, a,
                      (const double*)p->lqtab);
-  return hipGetLastError();
+  hipError_t e = hipGetLastError();
+  if (a.prof && e == hipSuccess) {
+    unsigned long long h[20];
+    (void)hipMemcpy(h, a.prof, sizeof(h), hipMemcpyDeviceToHost);
+    for (int ax = 0; ax < 2; ++ax) {
+      const unsigned long long* c = h + 10 * ax;
+      const double t = (double)(c[8] ? c[8] : 1), nt = (double)(c[9] ? c[9] : 1);
+      fprintf(stderr,
+              "lq prof axis %d: %llu tasks, %.0f clocks/task: sweep A tail %.3f, sweep A "
+              "working-set %.3f; sweep B working-set: set-up + checkpoint wait %.3f, Riccati "
+              "%.3f, forward %.3f, costate %.3f; sweep B tail %.3f; rest %.3f\n",
+              ax, c[9], t / nt, c[0] / t, c[1] / t, c[2] / t, c[4] / t, c[5] / t, c[6] / t,
+              c[7] / t, c[3] / t);
+    }
+  }
+  return e;
 }
 
 }  // namespace

@@ -55,6 +55,10 @@ inline T __shfl_up(T v, int d, int = 64) {
   return emu_xchg(v, l >= d ? l - d : l);
 }
 template <class T>
+inline T __shfl_xor(T v, int m, int = 64) {
+  return emu_xchg(v, (int)threadIdx.x ^ m);
+}
+template <class T>
 inline T __shfl(T v, int s, int = 64) {
   return emu_xchg(v, s);
 }

@@ -787,8 +787,9 @@ def test_strict_config3_full_size():
 
 def test_strict_shared_cop_full_size_properties():
     """Config 4 at its full per-GPU size (125 000 scenarios, shared CoP): every scenario's
-    status is 0, the x-axis rows are the same for every scenario, and translating the CoP
-    and the initial CoM by δ translates every CoM position by δ."""
+    status is 0, the x-axis rows are the same for every scenario, translating the CoP and the
+    initial CoM by δ translates every CoM position by δ, and 16 scenarios chosen by their lane
+    position — resident and queued tasks, the last block — equal the oracle's rollout."""
     d = golden("strict_ref.npz")
     zx, zn = d["n150_zmax"], d["n150_zmin"]
     n, dt = len(zx), 1.5 / 150
@@ -806,10 +807,57 @@ def test_strict_shared_cop_full_size_properties():
     assert float((h1[:, :, 0] - h1[0:1, :, 0]).abs().max()) <= 1e-12
     assert float(((h2 - h1)[..., 0] - delta).abs().max()) <= 1e-7
     assert float((h2 - h1)[..., 1:].abs().max()) <= 1e-5
-    # scenario 0 against the oracle (spot check inside the full-size launch)
-    ref = O.rollout_strict(np.zeros(3), np.zeros(3), zx, zn, 150, dt, H, G, Q, R,
-                           kick=float(kick[0]), kick_step=n // 2)
-    assert rmse(h1[0, :, :, 0].cpu().numpy(), ref[:, :, 0]) <= 1e-9
+    # scenarios by lane position in the kernel's kick order (order.hip: (kick step, float32
+    # kick), stable): the launch is 489 8-wave blocks (4 groups of 64 walks), the grid the
+    # resident blocks, the rest run as queued tasks — y waves first, then x waves.  Positions
+    # in the first and the last resident blocks, in queued blocks across the queue, and in the
+    # last block (walks 124 928 .. 124 999), each rolled by the oracle on its own kick.
+    import multiprocessing
+    from concurrent.futures import ProcessPoolExecutor
+    order = np.argsort((dt * F / M).astype(np.float32), kind="stable")  # position -> scenario
+    blocks = (B + 255) // 256
+    pos = [0, 255, 256 * 255 + 17, 256 * 256, 256 * 256 + 100, 256 * 300 + 63, 256 * 300 + 64,
+           256 * 350 + 200, 256 * 400 + 1, 256 * 450 + 128, 256 * 470 + 255, 256 * 480 + 64,
+           256 * (blocks - 2) + 190, 256 * (blocks - 1), 256 * (blocks - 1) + 37, B - 1]
+    walks = [int(order[q]) for q in pos]
+    h = h1[walks].cpu().numpy()
+    with ProcessPoolExecutor(max_workers=16,
+                             mp_context=multiprocessing.get_context("spawn")) as ex:
+        refs = list(ex.map(_oracle_strict_walk, [(zx, zn, float(kick[b]), n) for b in walks]))
+    for b, hb, ref in zip(walks, h, refs):
+        assert rmse(hb[:, :, 0], ref[:, :, 0]) <= 1e-9, b
+        assert np.abs(hb[:, 1] - ref[:, 1]).max() <= 1e-6, b
+
+
+def test_config5_full_size():
+    """BASELINE config 5 at its per-GPU size (16 384 walks over 8 GPUs = 2048 per GPU): N = 512,
+    dt = 1.5/512, n = 1431, default.json walks + rigid offsets, x0 and F_ext as SURVEY §8d —
+    the wide kernel with its launch geometry of the bench.  Translation invariance over the
+    whole batch (CoP and x0 + δ ⇒ every CoM position + δ), and 32 walks spread over the batch
+    equal the gain-form oracle (oracle.rollout_gain, zmp_controller.py:196-199)."""
+    B = 2048
+    zmax, zmin, x0, F, dt = synthetic_batch(B, 512)
+    n = zmax.shape[1]
+    assert n == 1431
+    kick = dt * F / M
+    p = plan(512, dt=dt)
+    zx_d = torch.as_tensor(zmax, device="cuda")
+    zn_d = torch.as_tensor(zmin, device="cuda")
+    x0_d = torch.as_tensor(x0, device="cuda")
+    kick_d = torch.as_tensor(kick, device="cuda")
+    h1, s1 = p.rollout(zx_d, zn_d, x0_d, kick=kick_d, kick_step=n // 2)
+    delta = 0.0625
+    x1 = x0_d.clone()
+    x1[:, :, 0] += delta
+    h2, s2 = p.rollout(zx_d + delta, zn_d + delta, x1, kick=kick_d, kick_step=n // 2)
+    assert int(s1.abs().max()) == 0 and int(s2.abs().max()) == 0
+    assert float(((h2 - h1)[..., 0] - delta).abs().max()) <= 1e-7
+    pick = np.unique(np.linspace(0, B - 1, 32).astype(int))
+    ref = O.rollout_gain(zmax[pick], zmin[pick], x0[pick], 512, dt, H, G, Q, R, kick[pick],
+                         n // 2)
+    h = h1[torch.as_tensor(pick, device="cuda")].cpu().numpy()
+    assert np.abs(h - ref).max() <= 1e-8
+    assert rmse(h[..., 0], ref[..., 0]) <= 1e-10
 
 
 # ------------------------------------------------ strict: long horizons, Cholesky cross-check
