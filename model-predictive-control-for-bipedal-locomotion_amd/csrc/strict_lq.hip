@@ -253,6 +253,33 @@ struct Flags {
   }
 };
 
+// A value function parked in the wave's LDS slot ([9][64] doubles).
+__device__ __forceinline__ void park(double* vp, const Ric& v, int lane) {
+  double* q = vp + lane;
+  q[0] = v.p00;
+  q[64] = v.p01;
+  q[128] = v.p02;
+  q[192] = v.p11;
+  q[256] = v.p12;
+  q[320] = v.p22;
+  q[384] = v.s0;
+  q[448] = v.s1;
+  q[512] = v.s2;
+}
+
+__device__ __forceinline__ void unpark(const double* vp, Ric& v, int lane) {
+  const double* q = vp + lane;
+  v.p00 = q[0];
+  v.p01 = q[64];
+  v.p02 = q[128];
+  v.p11 = q[192];
+  v.p12 = q[256];
+  v.p22 = q[320];
+  v.s0 = q[384];
+  v.s1 = q[448];
+  v.s2 = q[512];
+}
+
 // Issue the loads of segment j's slots (bounds, and the flags when FLAGS).  Slots past N read
 // padded rows (loaded, never used) so the loads carry no guards.
 template <int S, bool FLAGS>
@@ -418,21 +445,30 @@ __device__ __forceinline__ void seg_costate(const LqArgs& a, int j, const SegIn<
   }
 }
 
-// Sweep B through one working-set segment: Riccati from its checkpoint, forward, costate.
-// (lap: the diagnostics build's phase clock)
-template <int S, bool FULL, class Lap>
+// Sweep B through one working-set segment: Riccati from its checkpoint (in v), forward,
+// costate.  v is dead once the Riccati has run: `next` loads the next segment's checkpoint into
+// it there, so that the load is in flight under this segment's forward and costate.  (lap: the
+// diagnostics build's phase clock)
+template <int S, bool FULL, class Next, class Lap>
 __device__ __forceinline__ void seg_sweep_b(const LqArgs& a, int j, Ric& v, const SegIn<S>& in,
                                             SegOut<S>& g, double* xs, double& u0, bool& changed,
-                                            int& kl, const Flags& fl, int lane, Lap& lap) {
-  const Ric ve = v;  // V at the segment's end
+                                            int& kl, const Flags& fl, int lane, double* vpark,
+                                            Next& next, Lap& lap) {
+  // V at the segment's end, parked in LDS until the costate needs it (its registers hold the
+  // next checkpoint meanwhile)
+  park(vpark, v, lane);
   seg_riccati<S, FULL, true, false>(a, j, v, in, g);
+  next(v);
   lap(4);
   seg_forward<S, FULL>(a, j, in, g, xs, u0, changed, kl, fl, lane);
   lap(5);
   double lam[3];
-  lam[0] = fma(ve.p00, xs[0], fma(ve.p01, xs[1], ve.p02 * xs[2])) - ve.s0;
-  lam[1] = fma(ve.p01, xs[0], fma(ve.p11, xs[1], ve.p12 * xs[2])) - ve.s1;
-  lam[2] = fma(ve.p02, xs[0], fma(ve.p12, xs[1], ve.p22 * xs[2])) - ve.s2;
+  {
+    const double* q = vpark + lane;
+    lam[0] = fma(q[0], xs[0], fma(q[64], xs[1], q[128] * xs[2])) - q[384];
+    lam[1] = fma(q[64], xs[0], fma(q[192], xs[1], q[256] * xs[2])) - q[448];
+    lam[2] = fma(q[128], xs[0], fma(q[256], xs[1], q[320] * xs[2])) - q[512];
+  }
   seg_costate<S, FULL>(a, j, in, g, lam, changed, kl, fl, lane);
   lap(6);
 }
@@ -531,6 +567,9 @@ __global__ void __launch_bounds__(64 * G, 2)
   // slot flags [NS·S][64] bytes (rows past N stay 0: the last segment's loads are unguarded)
   const int fbytes = a.NS * S;
   const Flags fl{reinterpret_cast<signed char*>(lq_smem) + (size_t)wave * fbytes * 64};
+  // after the G waves' flags: each wave's parked V at the end of its current sweep-B segment
+  // ([9][64] doubles; 16-byte aligned: fbytes·64 is a multiple of 512)
+  double* vpark = reinterpret_cast<double*>(lq_smem + (size_t)G * fbytes * 64) + wave * 9 * 64;
   double* ck = a.ck + (size_t)gw * a.NS * kCkStride;
   const CkIO<NT> io{};
   // (per-lane counts in 32 bits: ≤ 2(n − 1)·64 passes and ·N slots per lane and task group)
@@ -564,7 +603,7 @@ __global__ void __launch_bounds__(64 * G, 2)
   const int64_t b = (valid && a.perm) ? (int64_t)a.perm[pos] : pos;
   Lane L;
   L.lane = lane;
-  L.col = RUNS ? lane : (int)(pos & 63);  // (pos = 64·group + lane; the forms allocate best)
+  L.col = RUNS ? lane : (int)(pos & 63);  // (pos = 64·group + lane; per form, as allocates best)
   {
     // the wave's (axis, group) tables; the run tables' base wave-uniform (SGPRs), the lane's
     // column added per access
@@ -653,6 +692,10 @@ __global__ void __launch_bounds__(64 * G, 2)
         SegOut<S> g;
         RunCursor rc{};
         if constexpr (RUNS) rc = run_bwd(L, ra);
+        // sweep B's first segment starts from V at the end of segment 0, which sweep A holds
+        // just before its last segment: parked in LDS (not stored), so that sweep B does not
+        // begin with a global load — one that would wait for every checkpoint store of sweep A
+        // (vmcnt counts loads and stores together, in issue order)
         // sweep A, free tail: the s recursion, checkpoints of s
 #pragma unroll 1
         for (int j = a.NS - 1; j >= jt; --j) {
@@ -660,7 +703,8 @@ __global__ void __launch_bounds__(64 * G, 2)
             seg_load_runs<S, false, false>(a, j, L, i, rc, fl, cur);
           else
             seg_load<S, false>(a, j, L, i, fl, cur);
-          ck_store_s(io, ck, j, v, lane);
+          if (j == 0) park(vpark, v, lane);
+          else ck_store_s(io, ck, j, v, lane);
           if (j < jfull)
             seg_tail<S, true, false>(a, tab, j, v, cur, g);
           else
@@ -683,7 +727,8 @@ __global__ void __launch_bounds__(64 * G, 2)
             seg_load_runs<S, true, false>(a, j, L, i, rc, fl, cur);
           else
             seg_load<S, true>(a, j, L, i, fl, cur);
-          ck_store(io, ck, j, v, lane);
+          if (j == 0) park(vpark, v, lane);
+          else ck_store(io, ck, j, v, lane);
           const bool fr = seg_free(cur);
           if (j < jfull) {
             if (fr)
@@ -708,17 +753,25 @@ __global__ void __launch_bounds__(64 * G, 2)
           xs[2] = xi2;
         }
         if constexpr (RUNS) rc = run_fwd(L, rb);
+        unpark(vpark, v, lane);  // V at the end of segment 0 (later segments' come by `next`)
+        // the next segment's checkpoint into v: full for a working-set segment, s for a tail one
+        auto next = [&](Ric& w, int j) {
+          if (j + 1 < jt)
+            ck_load(io, ck, j + 1, w, lane);
+          else if (j + 1 < a.NS)
+            ck_load_s(io, ck, j + 1, w, lane);
+        };
 #pragma unroll 1
         for (int j = 0; j < jt; ++j) {
           if constexpr (RUNS)
             seg_load_runs<S, true, true>(a, j, L, i, rc, fl, cur);
           else
             seg_load<S, true>(a, j, L, i, fl, cur);
-          ck_load(io, ck, j, v, lane);
           if (kLqProf && a.prof) {  // (diagnostics: the checkpoint's arrival timed apart)
             __builtin_amdgcn_s_waitcnt(0);
             lap(2);
           }
+          auto nx = [&](Ric& w) { next(w, j); };
 #ifdef ZMPC_DIAG
           ++n_sb_ws;  // diagnostics: sweep-B working-set segments, and those no lane pins
           if (seg_free(cur)) ++n_sb_free;
@@ -728,23 +781,26 @@ __global__ void __launch_bounds__(64 * G, 2)
           // costate — spills at 256 VGPRs: 74.9 vs 65.0 ms, and 66.7 ms at S = 6,
           // profiles/r4/r4n/)
           if (j < jfull) {
-            seg_sweep_b<S, true>(a, j, v, cur, g, xs, u0, changed, kl, fl, lane, lap);
+            seg_sweep_b<S, true>(a, j, v, cur, g, xs, u0, changed, kl, fl, lane, vpark, nx,
+                                 lap);
           } else {
-            seg_sweep_b<S, false>(a, j, v, cur, g, xs, u0, changed, kl, fl, lane, lap);
+            seg_sweep_b<S, false>(a, j, v, cur, g, xs, u0, changed, kl, fl, lane, vpark, nx,
+                                  lap);
           }
         }
 #pragma unroll 1
-        for (int j = jt; j < a.NS; ++j) {
+        for (int j = jt; j < a.NS; ++j) {  // (v.s holds the segment's checkpoint: `next`)
           if constexpr (RUNS)
             seg_load_runs<S, false, true>(a, j, L, i, rc, fl, cur);
           else
             seg_load<S, false>(a, j, L, i, fl, cur);
-          ck_load_s(io, ck, j, v, lane);
           if (j < jfull) {
             seg_tail<S, true, true>(a, tab, j, v, cur, g);
+            next(v, j);  // (s is dead after the segment's recursion)
             seg_forward_tail<S, true>(a, tab, j, cur, g, xs, u0, changed, kl, fl, lane);
           } else {
             seg_tail<S, false, true>(a, tab, j, v, cur, g);
+            next(v, j);
             seg_forward_tail<S, false>(a, tab, j, cur, g, xs, u0, changed, kl, fl, lane);
           }
         }
@@ -1012,10 +1068,10 @@ const LqVariant kLqVariants[] = {
 #undef ZMPC_LQK
 constexpr size_t kLdsCap = 160 * 1024;
 
-// LDS of one workgroup: the G waves' slot flags.
+// LDS of one workgroup: the G waves' slot flags and parked V ([9][64] doubles each).
 size_t lq_lds_bytes(int G, int N) {
   const size_t rows = (size_t)(N + LQ_S - 1) / LQ_S * LQ_S;
-  return (size_t)G * rows * 64;
+  return (size_t)G * (rows * 64 + 9 * 64 * sizeof(double));
 }
 
 // The largest workgroup whose slot flags fit a CU (N ≤ 2560 at G = 1).

@@ -285,7 +285,7 @@ __device__ __forceinline__ void shfl_down_elem(const Elem& e, Elem& o, int d) {
 // has converged keeps its working set while the others of its wave iterate (a converged set
 // reproduces itself, so its extra passes change nothing; they are not counted).
 template <int C, int L>
-__global__ void __launch_bounds__(64, 2) zmpc_strict_scan_kernel(ScanArgs a) {
+__global__ void __launch_bounds__(64, (C >= 4 ? 1 : 2)) zmpc_strict_scan_kernel(ScanArgs a) {
   static_assert(L == 64 || L == 32 || L == 16, "lanes per instance");
   const int lane = threadIdx.x;
   const int il = lane & (L - 1);     // lane within the instance
@@ -318,8 +318,8 @@ __global__ void __launch_bounds__(64, 2) zmpc_strict_scan_kernel(ScanArgs a) {
 #pragma unroll
   for (int q = 0; q < C; ++q) f[q] = 0;
   int fq = 0;
-  unsigned long long passes = 0;   // the instance's passes (counters [1], [2])
-  unsigned long long wpasses = 0;  // the wave's passes: per timestep the most of its instances
+  unsigned passes = 0;   // the instance's passes (counters [1], [2])
+  unsigned wpasses = 0;  // the wave's passes: per timestep the most of its instances
   unsigned itmax = 0;
   const unsigned long long imask = (L == 64) ? ~0ull : (((1ull << L) - 1) << base);
 
@@ -539,12 +539,12 @@ __global__ void __launch_bounds__(64, 2) zmpc_strict_scan_kernel(ScanArgs a) {
       }
       again = __any(mine);
     }
-    passes += (unsigned long long)it;
+    passes += (unsigned)it;
     itmax = max(itmax, (unsigned)it);
     {
       int wit = it;  // (lanes of one instance hold the same count)
       for (int o = L; o < 64; o <<= 1) wit = max(wit, __shfl_xor(wit, o, 64));
-      wpasses += (unsigned long long)wit;
+      wpasses += (unsigned)wit;
     }
     // converged: advance in the reference form x⁺ = A x + B u0 (zmp_controller.py:199)
     const double u0 = __shfl(v0, base, 64) / a.Tcu;
@@ -585,9 +585,9 @@ __global__ void __launch_bounds__(64, 2) zmpc_strict_scan_kernel(ScanArgs a) {
         atomicOr(&a.status[b], fq);
     }
     if (a.cnt) {
-      if (lane == 0) atomicAdd(a.cnt + 0, wpasses);  // once per wave
-      atomicAdd(a.cnt + 1, passes);
-      atomicAdd(a.cnt + 2, passes * (unsigned long long)N);
+      if (lane == 0) atomicAdd(a.cnt + 0, (unsigned long long)wpasses);  // once per wave
+      atomicAdd(a.cnt + 1, (unsigned long long)passes);
+      atomicAdd(a.cnt + 2, (unsigned long long)passes * (unsigned long long)N);
       atomicMax(a.cnt + 8, (unsigned long long)itmax);
     }
   }
@@ -614,11 +614,15 @@ void fill(const zmpc_plan* p, ScanArgs& a) {
 }
 
 // Lanes per instance: a whole wave while the instances fit the chip's resident waves (the
-// latency of one pass is what counts), 32 beyond (half the waves; the chunks of up to 8 slots
-// keep N ≤ 256 in registers).
+// latency of one pass is what counts), 32 beyond (half the waves; chunks of up to 10 slots,
+// N ≤ 320).  Chunks of C ≥ 4 slots per lane hold 1 wave per SIMD (their state
+// spills past 256 VGPRs into AGPRs instead of scratch: __launch_bounds__ above), shorter ones 2.
+int waves_per_simd(int C) { return C >= 4 ? 1 : 2; }
+
 int lanes_per_instance(const zmpc_plan* p, int64_t ninst) {
-  const int64_t resident = (int64_t)(p->cus > 0 ? p->cus : 256) * 4 * 2;  // 2 waves per SIMD
-  return (ninst > resident && p->N <= 256) ? 32 : 64;
+  const int64_t cus = p->cus > 0 ? p->cus : 256;
+  const int64_t resident = cus * 4 * waves_per_simd((p->N + 63) / 64);
+  return (ninst > resident && p->N <= 320) ? 32 : 64;
 }
 
 hipError_t launch(const zmpc_plan* p, const ScanArgs& a, hipStream_t s, int L) {
@@ -631,7 +635,7 @@ hipError_t launch(const zmpc_plan* p, const ScanArgs& a, hipStream_t s, int L) {
     hipLaunchKernelGGL((zmpc_strict_scan_kernel<CC, 32>), grid, blk, 0, s, a); \
     break;
       ZMPC_SCASE(1) ZMPC_SCASE(2) ZMPC_SCASE(3) ZMPC_SCASE(4) ZMPC_SCASE(5) ZMPC_SCASE(6)
-      ZMPC_SCASE(7) ZMPC_SCASE(8)
+      ZMPC_SCASE(7) ZMPC_SCASE(8) ZMPC_SCASE(9) ZMPC_SCASE(10)
 #undef ZMPC_SCASE
       default:
         return hipErrorInvalidValue;

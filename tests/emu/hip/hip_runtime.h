@@ -1,5 +1,6 @@
-// Host emulation of the few HIP device facilities strict_scan.hip's kernel uses, for the CPU
-// test of its wave-level logic (tests/test_scan_emulation.py).  Test infrastructure only.
+// Host emulation of the few HIP device facilities the strict kernels use (strict_scan.hip,
+// strict_lq.hip), for the CPU tests of their wave-level logic (tests/test_scan_emulation.py,
+// tests/test_lq_emulation.py).  Test infrastructure only.
 // One wave = 64 lanes run as stackful coroutines (ucontext) in one thread; every cross-lane
 // operation (shuffles, __any) is a lockstep point: each lane publishes its value and yields,
 // and reads once every lane has published.  Correct for kernels whose cross-lane operations
@@ -93,6 +94,28 @@ inline unsigned long long atomicMax(unsigned long long* p, unsigned long long v)
   *p = std::max(*p, v);
   return o;
 }
+inline int atomicAdd(int* p, int v) {
+  const int o = *p;
+  *p += v;
+  return o;
+}
+// (strict_lq.hip) wave-uniform values, scheduling hints, cache policy: no-ops on the host
+inline int __builtin_amdgcn_readfirstlane(int v) { return v; }
+inline void __builtin_amdgcn_sched_barrier(int) {}
+inline void __builtin_amdgcn_s_waitcnt(int) {}
+#define __builtin_nontemporal_store(v, p) (*(p) = (v))
+#define __builtin_nontemporal_load(p) (*(p))
+inline unsigned long long clock64() { return 0; }
+#define __shared__
+inline void __syncthreads() {}  // (the row-staging kernel, which the emulation does not run)
+struct dim3 {
+  unsigned x, y, z;
+  dim3(unsigned a = 1, unsigned b = 1, unsigned c = 1) : x(a), y(b), z(c) {}
+};
+struct double2 {
+  double x, y;
+};
+inline double2 make_double2(double x, double y) { return double2{x, y}; }
 #define hipLaunchKernelGGL(...) (void)0
 inline hipError_t hipGetLastError() { return 0; }
 inline hipError_t hipMemsetAsync(void*, int, size_t, hipStream_t) { return 0; }

@@ -1008,11 +1008,12 @@ def test_strict_small_and_large_batch_paths_agree(B, auto):
 
 
 @pytest.mark.parametrize("N,B", ((1, 3), (2, 5), (63, 7), (65, 7), (129, 1100), (257, 5),
-                                 (512, 3)))
+                                 (300, 600), (512, 3)))
 def test_strict_scan_kernel_chunk_widths(N, B):
     """The parallel-in-time kernel at the edges of its chunk widths (C = ⌈N/64⌉ = 1..8 slots
     per lane; N = 65/129 leave the last lane one slot, N = 1 a single lane) and with 32 lanes per
-    instance (B = 1100 walks: 2200 instances beyond the resident waves) against the LQ kernel on
+    instance (B = 1100 walks: 2200 instances beyond the resident waves; N = 300, B = 600: 10 slots
+    per lane of 32, one wave per SIMD) against the LQ kernel on
     the same kicked walks: CoM within 1e-9, same statuses; and one window-mode step."""
     zmax, zmin, x0, F, dt = synthetic_batch(B, 64 if N < 150 else 150, seed=N)
     n = zmax.shape[1]

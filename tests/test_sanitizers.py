@@ -86,3 +86,17 @@ def test_scan_kernel_emulation_sanitized(tmp_path):
     assert err.strip().endswith("status 0"), err[-2000:]
     h = np.frombuffer(r.stdout, np.float64).reshape(n, 2, 3)
     assert np.abs(h[:, :, 0] - s[f"n{N}_F800_com"]).max() <= 1e-12
+
+
+def test_lq_kernel_emulation_sanitized(tmp_path):
+    """The strict LQ kernel's source (staging, free-tail table, the kernel) on the host
+    emulation under ASan/UBSan (tests/test_lq_emulation.py's build), one kicked walk."""
+    from test_lq_emulation import build_lq_emulator, run_lq
+    exe = build_lq_emulator(tmp_path, (*SAN, "-DEMU_STACK_SHIFT=17"))
+    s = golden("strict_ref.npz")
+    N, F = 64, 800.0
+    zx, zn = s[f"n{N}_zmax"], s[f"n{N}_zmin"]
+    n = len(zx)
+    env = dict(ENV, ASAN_OPTIONS=ENV["ASAN_OPTIONS"] + ":detect_stack_use_after_return=0")
+    h = run_lq(tmp_path, exe, zx, zn, N, np.zeros(6), (1.5 / N) * F / 40.0, n // 2, env=env)
+    assert np.abs(h[:, :, 0] - s[f"n{N}_F800_com"]).max() <= 1e-12
