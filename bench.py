@@ -170,6 +170,7 @@ def herdt_bench(args, rank, world, dev, dist_on):
     flops = float(N * (160 * P + 26 * Sm + 2 * Sm2)) / args.steps
     tfs = flops / (kern_ms * 1e-3) / 1e12
     passes_per_solve = P / (args.steps * 2 * B * (n - 1))
+    alg_bytes = B * n * (6 + 2) * 8 + B * (6 + 1) * 8 + n * (2 * 8 + 1 + 4)
     if rank != 0:
         return None
     com_rmse_ref = None
@@ -199,6 +200,12 @@ def herdt_bench(args, rank, world, dev, dist_on):
                      "frac": tfs / FP64_PEAK_TFS, "traffic": pmc_traffic(f"config6_n{N}_b{B}"),
                      "kernel": "zmpc_herdt_kernel", "kernel_ms": kern_ms,
                      "alg_flops_per_launch": flops,
+                     # compulsory bytes: the history [B,n,2,3] and foot track [B,n,2] out, x0 and
+                     # the kick in, the shared v_ref / states / footstep counters once
+                     "alg_bytes_per_launch": alg_bytes,
+                     "traffic_over_alg_bytes": (None if not pmc_traffic(f"config6_n{N}_b{B}")
+                                                else pmc_traffic(f"config6_n{N}_b{B}") /
+                                                alg_bytes),
                      "passes_per_solve": passes_per_solve,
                      "max_passes_per_solve": cnt["herdt_max_passes_per_solve"],
                      "wave_passes_per_launch": cnt["herdt_wave_passes"] / args.steps,

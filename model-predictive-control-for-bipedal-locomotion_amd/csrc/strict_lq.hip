@@ -46,6 +46,7 @@
 #include <cstdio>
 #include <cstring>
 #include <cstdlib>
+#include <type_traits>
 
 #include "strict_eta.h"
 #include "zmpc_internal.h"
@@ -449,16 +450,20 @@ __device__ __forceinline__ void seg_costate(const LqArgs& a, int j, const SegIn<
 // costate.  v is dead once the Riccati has run: `next` loads the next segment's checkpoint into
 // it there, so that the load is in flight under this segment's forward and costate.  (lap: the
 // diagnostics build's phase clock)
-template <int S, bool FULL, class Next, class Lap>
+// RECOMP = false: the feedback is already in g and V at the segment's end parked (segment 0,
+// from sweep A).
+template <int S, bool FULL, bool RECOMP, class Next, class Lap>
 __device__ __forceinline__ void seg_sweep_b(const LqArgs& a, int j, Ric& v, const SegIn<S>& in,
                                             SegOut<S>& g, double* xs, double& u0, bool& changed,
                                             int& kl, const Flags& fl, int lane, double* vpark,
                                             Next& next, Lap& lap) {
-  // V at the segment's end, parked in LDS until the costate needs it (its registers hold the
-  // next checkpoint meanwhile)
-  park(vpark, v, lane);
-  seg_riccati<S, FULL, true, false>(a, j, v, in, g);
-  next(v);
+  if constexpr (RECOMP) {
+    // V at the segment's end, parked in LDS until the costate needs it (its registers hold the
+    // next checkpoint meanwhile)
+    park(vpark, v, lane);
+    seg_riccati<S, FULL, true, false>(a, j, v, in, g);
+    next(v);
+  }
   lap(4);
   seg_forward<S, FULL>(a, j, in, g, xs, u0, changed, kl, fl, lane);
   lap(5);
@@ -569,7 +574,10 @@ __global__ void __launch_bounds__(64 * G, 2)
   const Flags fl{reinterpret_cast<signed char*>(lq_smem) + (size_t)wave * fbytes * 64};
   // after the G waves' flags: each wave's parked V at the end of its current sweep-B segment
   // ([9][64] doubles; 16-byte aligned: fbytes·64 is a multiple of 512)
-  double* vpark = reinterpret_cast<double*>(lq_smem + (size_t)G * fbytes * 64) + wave * 9 * 64;
+  double* vpark = reinterpret_cast<double*>(lq_smem + (size_t)G * fbytes * 64) + wave * 12 * 64;
+  // and behind it the lane's state x (the reference form), [3][64]: read at a pass's start and
+  // at its end only, so it need not hold registers through the sweeps
+  double* xpark = vpark + 9 * 64;
   double* ck = a.ck + (size_t)gw * a.NS * kCkStride;
   const CkIO<NT> io{};
   // (per-lane counts in 32 bits: ≤ 2(n − 1)·64 passes and ·N slots per lane and task group)
@@ -630,31 +638,35 @@ __global__ void __launch_bounds__(64 * G, 2)
   const int jfull = N / S;  // segments [0, jfull) are full
   for (int k = 0; k < fbytes; ++k) fl.p[k * 64 + lane] = 0;
 
-  double x[3] = {0.0, 0.0, 0.0};
-  if (valid) {
-    const double* xp = a.window_mode ? a.x0 + b * 3 : a.x0 + (b * 2 + axis) * 3;
-    x[0] = xp[0];
-    x[1] = xp[1];
-    x[2] = xp[2];
-    if (!a.window_mode) {
-      double* h = a.out + ((b * a.n) * 2 + axis) * 3;  // hist[b, 0, axis, :] = x0
-      h[0] = x[0];
-      h[1] = x[1];
-      h[2] = x[2];
+  {
+    double x[3] = {0.0, 0.0, 0.0};
+    if (valid) {
+      const double* xp = a.window_mode ? a.x0 + b * 3 : a.x0 + (b * 2 + axis) * 3;
+      x[0] = xp[0];
+      x[1] = xp[1];
+      x[2] = xp[2];
+      if (!a.window_mode) {
+        double* h = a.out + ((b * a.n) * 2 + axis) * 3;  // hist[b, 0, axis, :] = x0
+        h[0] = x[0];
+        h[1] = x[1];
+        h[2] = x[2];
+      }
     }
+    xpark[lane] = x[0];
+    xpark[64 + lane] = x[1];
+    xpark[128 + lane] = x[2];
   }
   int fq = 0;
   const int kstep =
       (!a.window_mode && axis == 1 && a.kick != nullptr && valid)
           ? (int)(a.kick_steps ? a.kick_steps[b] : a.kick_step)
           : -1;
-  const double kv = (kstep >= 0) ? a.kick[b] : 0.0;
 
   // Each lane walks its own timestep i: a pass runs for every lane still inside its rollout
   // and at most LQ_DRIFT timesteps ahead of the wave's slowest lane (so a slot's bound loads
   // stay within a few 1-KiB rows); a lane whose working set repeated advances (state, history,
   // shifted warm start) while the others keep iterating.
-  int64_t i = 0;
+  int i = 0;  // (the lane's timestep; n < 2^31)
   bool active = valid && a.nsteps > 0;
   int it = 0;
   int klast = -1;      // last pinned slot of this lane's working set (−1: none)
@@ -674,7 +686,7 @@ __global__ void __launch_bounds__(64 * G, 2)
     ++n_wave_pass;
     int imin = active ? (int)i : 0x7fffffff;
     for (int o = 32; o > 0; o >>= 1) imin = min(imin, __shfl_xor(imin, o));
-    const bool part = active && i <= (int64_t)imin + LQ_DRIFT;
+    const bool part = active && i <= imin + LQ_DRIFT;
     // segments [jt, NS) hold no pinned slot of any lane taking part: the free tail
     int kw = part ? klast : -1;
     for (int o = 32; o > 0; o >>= 1) kw = max(kw, __shfl_xor(kw, o));
@@ -722,13 +734,12 @@ __global__ void __launch_bounds__(64 * G, 2)
         }
         // sweep A, working-set segments: full Riccati, checkpoints of (P, s)
 #pragma unroll 1
-        for (int j = jt - 1; j >= 0; --j) {
+        for (int j = jt - 1; j >= 1; --j) {
           if constexpr (RUNS)
             seg_load_runs<S, true, false>(a, j, L, i, rc, fl, cur);
           else
             seg_load<S, true>(a, j, L, i, fl, cur);
-          if (j == 0) park(vpark, v, lane);
-          else ck_store(io, ck, j, v, lane);
+          ck_store(io, ck, j, v, lane);
           const bool fr = seg_free(cur);
           if (j < jfull) {
             if (fr)
@@ -742,18 +753,31 @@ __global__ void __launch_bounds__(64 * G, 2)
               seg_riccati<S, false, false, false>(a, j, v, cur, g);
           }
         }
+        // segment 0, its feedback kept: it is sweep B's first segment, which then needs no
+        // recompute (its V at the end parked for the costate)
+        if (jt > 0) {
+          if constexpr (RUNS)
+            seg_load_runs<S, true, false>(a, 0, L, i, rc, fl, cur);
+          else
+            seg_load<S, true>(a, 0, L, i, fl, cur);
+          park(vpark, v, lane);
+          if (0 < jfull)
+            seg_riccati<S, true, true, false>(a, 0, v, cur, g);
+          else
+            seg_riccati<S, false, true, false>(a, 0, v, cur, g);
+        }
         lap(1);
         // sweep B: per segment from the front — recompute its steps from the checkpoint,
         // forward, then (working-set segments) the costate back through it
         double xs[3];  // η
         {
-          const double xi1 = a.T * x[1], xi2 = a.Tsq * x[2];  // ξ
-          xs[0] = fma(-1.0 / 6.0, xi2, x[0]);
+          const double x0 = xpark[lane], x1 = xpark[64 + lane], x2 = xpark[128 + lane];
+          const double xi1 = a.T * x1, xi2 = a.Tsq * x2;  // ξ
+          xs[0] = fma(-1.0 / 6.0, xi2, x0);
           xs[1] = fma(-0.5, xi2, xi1);
           xs[2] = xi2;
         }
         if constexpr (RUNS) rc = run_fwd(L, rb);
-        unpark(vpark, v, lane);  // V at the end of segment 0 (later segments' come by `next`)
         // the next segment's checkpoint into v: full for a working-set segment, s for a tail one
         auto next = [&](Ric& w, int j) {
           if (j + 1 < jt)
@@ -761,8 +785,15 @@ __global__ void __launch_bounds__(64 * G, 2)
           else if (j + 1 < a.NS)
             ck_load_s(io, ck, j + 1, w, lane);
         };
-#pragma unroll 1
-        for (int j = 0; j < jt; ++j) {
+        // V at the end of segment 0 (later segments' come by `next`); with working-set segments
+        // sweep A has left segment 0's feedback in g and V at its end parked: the checkpoint of
+        // segment 1 can be in flight from here
+        if (jt > 0)
+          next(v, 0);
+        else
+          unpark(vpark, v, lane);
+        // one working-set segment of sweep B (R: recompute its feedback from the checkpoint)
+        auto seg_b = [&](int j, auto R) {
           if constexpr (RUNS)
             seg_load_runs<S, true, true>(a, j, L, i, rc, fl, cur);
           else
@@ -781,13 +812,16 @@ __global__ void __launch_bounds__(64 * G, 2)
           // costate — spills at 256 VGPRs: 74.9 vs 65.0 ms, and 66.7 ms at S = 6,
           // profiles/r4/r4n/)
           if (j < jfull) {
-            seg_sweep_b<S, true>(a, j, v, cur, g, xs, u0, changed, kl, fl, lane, vpark, nx,
-                                 lap);
+            seg_sweep_b<S, true, decltype(R)::value>(a, j, v, cur, g, xs, u0, changed, kl, fl,
+                                                     lane, vpark, nx, lap);
           } else {
-            seg_sweep_b<S, false>(a, j, v, cur, g, xs, u0, changed, kl, fl, lane, vpark, nx,
-                                  lap);
+            seg_sweep_b<S, false, decltype(R)::value>(a, j, v, cur, g, xs, u0, changed, kl, fl,
+                                                      lane, vpark, nx, lap);
           }
-        }
+        };
+        if (jt > 0) seg_b(0, std::false_type{});  // (sweep A's feedback)
+#pragma unroll 1
+        for (int j = 1; j < jt; ++j) seg_b(j, std::true_type{});
 #pragma unroll 1
         for (int j = jt; j < a.NS; ++j) {  // (v.s holds the segment's checkpoint: `next`)
           if constexpr (RUNS)
@@ -816,15 +850,16 @@ __global__ void __launch_bounds__(64 * G, 2)
         // converged: advance in the reference form x⁺ = A x + B u0 (zmp_controller.py:199)
         u0 = u0 / a.Tcu;  // v0 = T³ u0
         double xn[3];
-        xn[0] = x[0] + a.T * x[1] + a.T2 * x[2] + a.T3 * u0;
-        xn[1] = x[1] + a.T * x[2] + a.T2 * u0;
-        xn[2] = x[2] + a.T * u0;
-        if ((int)i == kstep) xn[1] -= kv;  // force kick (zmp_controller.py:90,105-106)
+        const double x0 = xpark[lane], x1 = xpark[64 + lane], x2 = xpark[128 + lane];
+        xn[0] = x0 + a.T * x1 + a.T2 * x2 + a.T3 * u0;
+        xn[1] = x1 + a.T * x2 + a.T2 * u0;
+        xn[2] = x2 + a.T * u0;
+        if ((int)i == kstep) xn[1] -= a.kick[b];  // force kick (zmp_controller.py:90,105-106)
         if (!(isfinite(xn[0]) && isfinite(xn[1]) && isfinite(xn[2]))) fq |= ZMPC_ST_NONFINITE;
-        x[0] = xn[0];
-        x[1] = xn[1];
-        x[2] = xn[2];
-        double* h = a.window_mode ? a.out + b * 3 : a.out + ((b * a.n + i + 1) * 2 + axis) * 3;
+        xpark[lane] = xn[0];
+        xpark[64 + lane] = xn[1];
+        xpark[128 + lane] = xn[2];
+        double* h = a.window_mode ? a.out + b * 3 : a.out + ((b * a.n + (int64_t)i + 1) * 2 + axis) * 3;
         h[0] = xn[0];
         h[1] = xn[1];
         h[2] = xn[2];
@@ -1068,10 +1103,10 @@ const LqVariant kLqVariants[] = {
 #undef ZMPC_LQK
 constexpr size_t kLdsCap = 160 * 1024;
 
-// LDS of one workgroup: the G waves' slot flags and parked V ([9][64] doubles each).
+// LDS of one workgroup: the G waves' slot flags, parked V and state ([12][64] doubles each).
 size_t lq_lds_bytes(int G, int N) {
   const size_t rows = (size_t)(N + LQ_S - 1) / LQ_S * LQ_S;
-  return (size_t)G * (rows * 64 + 9 * 64 * sizeof(double));
+  return (size_t)G * (rows * 64 + 12 * 64 * sizeof(double));
 }
 
 // The largest workgroup whose slot flags fit a CU (N ≤ 2560 at G = 1).
@@ -1097,7 +1132,10 @@ hipError_t launch_lq(const zmpc_plan* p, LqArgs& a, int64_t waves, hipStream_t s
   const int64_t blocks = (waves + var->G - 1) / var->G;
   const size_t lds = lq_lds_bytes(var->G, p->N);
   // rollouts over per-walk bounds: non-temporal checkpoints (see CkIO)
-  const bool nt = !a.window_mode && !a.shared;
+  bool nt = !a.window_mode && !a.shared;
+#ifdef ZMPC_DIAG
+  if (const char* e = getenv("ZMPC_LQ_NT")) nt = atoi(e) != 0;  // (diagnostics: A/B of the policy)
+#endif
   auto k = a.rs ? (nt ? var->kernel_runs_nt : var->kernel_runs) : (nt ? var->kernel_nt : var->kernel);
   auto kq = a.rs ? (nt ? var->q_kernel_runs_nt : var->q_kernel_runs)
                  : (nt ? var->q_kernel_nt : var->q_kernel);
