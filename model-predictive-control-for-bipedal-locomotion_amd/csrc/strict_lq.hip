@@ -125,8 +125,11 @@ struct LqArgs {
 
 template <int S>
 struct SegIn {  // a segment's window slots: z_ref, half-width of the box, working-set flags
+  static_assert(S <= 8, "a segment's flags are one 8-byte word");
   double r[S], h[S];
-  int f[S];  // 0 free, +1 at z_max = r + h, −1 at z_min = r − h
+  unsigned long long fw;  // the flags, one signed byte per slot: 0 free, +1 at z_max = r + h,
+                          // −1 at z_min = r − h
+  __device__ __forceinline__ int f(int q) const { return (int)(signed char)(fw >> (8 * q)); }
 };
 
 template <int S>
@@ -245,12 +248,23 @@ __device__ __forceinline__ void seg_runs(const Lane& L, int t0, RunCursor& c, do
 }
 
 // Per-lane working-set flags of the wave's N slots in LDS (0 free, +1 at z_max, −1 at z_min):
-// one signed byte per slot, [slot][64].
+// one signed byte per slot, [slot / 8][64 lanes][8], so that a lane's segment of 8 slots is one
+// 8-byte word (one conflict-free ds_read_b64 per segment, held packed in the registers).
 struct Flags {
   signed char* p;
-  __device__ __forceinline__ int get(int k, int lane) const { return p[k * 64 + lane]; }
+  __device__ __forceinline__ static int at(int k, int lane) {
+    return ((k >> 3) * 64 + lane) * 8 + (k & 7);
+  }
+  __device__ __forceinline__ int get(int k, int lane) const { return p[at(k, lane)]; }
   __device__ __forceinline__ void set(int k, int lane, int v) const {
-    p[k * 64 + lane] = (signed char)v;
+    p[at(k, lane)] = (signed char)v;
+  }
+  // the 8 flags of slots 8c .. 8c + 7
+  __device__ __forceinline__ unsigned long long word(int c, int lane) const {
+    return *reinterpret_cast<const unsigned long long*>(p + (c * 64 + lane) * 8);
+  }
+  __device__ __forceinline__ void set_word(int c, int lane, unsigned long long w) const {
+    *reinterpret_cast<unsigned long long*>(p + (c * 64 + lane) * 8) = w;
   }
 };
 
@@ -281,6 +295,21 @@ __device__ __forceinline__ void unpark(const double* vp, Ric& v, int lane) {
   v.s2 = q[512];
 }
 
+// A segment's flags as one word (S = 8: segment j is flag word j; a shorter segment gathers
+// its bytes).
+template <int S>
+__device__ __forceinline__ unsigned long long seg_flags(const Flags& fl, int j, int lane) {
+  if constexpr (S == 8) {
+    return fl.word(j, lane);
+  } else {
+    unsigned long long w = 0;
+#pragma unroll
+    for (int q = 0; q < S; ++q)
+      w |= (unsigned long long)(unsigned char)fl.get(j * S + q, lane) << (8 * q);
+    return w;
+  }
+}
+
 // Issue the loads of segment j's slots (bounds, and the flags when FLAGS).  Slots past N read
 // padded rows (loaded, never used) so the loads carry no guards.
 template <int S, bool FLAGS>
@@ -295,8 +324,8 @@ __device__ __forceinline__ void seg_load(const LqArgs& a, int j, const Lane& L, 
     const double2 v = hp[q * 64 + L.col];
     in.r[q] = v.x;
     in.h[q] = v.y;
-    if (FLAGS) in.f[q] = fl.get(j * S + q, L.lane);
   }
+  if (FLAGS) in.fw = seg_flags<S>(fl, j, L.lane);
 }
 
 // The same from the run lists (RUNS): bounds from the lane's cursor, flags from LDS.
@@ -304,19 +333,13 @@ template <int S, bool FLAGS, bool FWD>
 __device__ __forceinline__ void seg_load_runs(const LqArgs& a, int j, const Lane& L, int64_t i,
                                               RunCursor& c, const Flags& fl, SegIn<S>& in) {
   seg_runs<S, FWD>(L, (int)(i + a.toff) + j * S, c, in.r, in.h);
-  if (FLAGS) {
-#pragma unroll
-    for (int q = 0; q < S; ++q) in.f[q] = fl.get(j * S + q, L.lane);
-  }
+  if (FLAGS) in.fw = seg_flags<S>(fl, j, L.lane);
 }
 
 // No lane taking part has a pinned slot in the segment (wave-uniform).
 template <int S>
 __device__ __forceinline__ bool seg_free(const SegIn<S>& in) {
-  int any = 0;
-#pragma unroll
-  for (int q = 0; q < S; ++q) any |= in.f[q];
-  return !__any(any != 0);
+  return !__any(in.fw != 0);
 }
 
 // Riccati steps of segment j (slots jS + S−1 down to jS).  KEEP: feedback kept in g (sweep
@@ -334,7 +357,7 @@ __device__ __forceinline__ void seg_riccati(const LqArgs& a, int j, Ric& v, cons
         double iq, u0, u1, u2;
         ric_free(a, v, in.r[q], K0, K1, K2, kf, iq, u0, u1, u2);
       } else {
-        ric_step(a, v, in.r[q], in.h[q], in.f[q], K0, K1, K2, kf);
+        ric_step(a, v, in.r[q], in.h[q], in.f(q), K0, K1, K2, kf);
       }
       if (KEEP) {
         g.K0[q] = K0;
@@ -384,7 +407,7 @@ __device__ __forceinline__ void seg_forward(const LqArgs& a, int j, const SegIn<
       const double d = z - in.r[q], ht = in.h[q] + tol;
       g.w[q] = u;
       const int nf = (d > ht) ? 1 : ((d < -ht) ? -1 : 0);
-      if (in.f[q] == 0) {
+      if (in.f(q) == 0) {
         fl.set(k, lane, nf);
         changed |= nf != 0;
         kl = nf ? k : kl;  // (slots ascend)
@@ -429,7 +452,7 @@ __device__ __forceinline__ void seg_costate(const LqArgs& a, int j, const SegIn<
   for (int q = S - 1; q >= 0; --q) {
     const int k = j * S + q;
     if (FULL || k < a.N) {
-      const int f = in.f[q];
+      const int f = in.f(q);
       {
         const double sg = (double)f;
         const double nu = pinned_nu(a, sg, in.h[q], g.w[q], lam);  // ν / Q (pinned slots only)
@@ -636,7 +659,7 @@ __global__ void __launch_bounds__(64 * G, 2)
     while (L.rt[(rb + 1) * 64 + L.col] <= tB) ++rb;
   }
   const int jfull = N / S;  // segments [0, jfull) are full
-  for (int k = 0; k < fbytes; ++k) fl.p[k * 64 + lane] = 0;
+  for (int c = 0; c < fbytes / 8; ++c) fl.set_word(c, lane, 0ull);
 
   {
     double x[3] = {0.0, 0.0, 0.0};
@@ -873,8 +896,18 @@ __global__ void __launch_bounds__(64 * G, 2)
         if (i < a.nsteps) {
           // warm start: the converged set shifted one slot towards the present (slot N−1
           // kept), this lane's column only
-#pragma unroll 8
-          for (int k = 0; k < N - 1; ++k) fl.p[k * 64 + lane] = fl.p[(k + 1) * 64 + lane];
+          // (flag words: each word takes its upper 7 bytes and the next word's first)
+          {
+            const signed char keep = fl.get(N - 1, lane);
+            const int nw = fbytes / 8;
+            unsigned long long w = fl.word(0, lane);
+            for (int c = 0; c < nw; ++c) {
+              const unsigned long long nx = (c + 1 < nw) ? fl.word(c + 1, lane) : 0ull;
+              fl.set_word(c, lane, (w >> 8) | (nx << 56));
+              w = nx;
+            }
+            fl.set(N - 1, lane, keep);
+          }
           // the previous solve's terminal slot is no longer terminal: it starts free (its end
           // effect pinned it more often than the next solve keeps it; a CPU simulation of this
           // iteration on the default walk's y axis at F_ext 0/400/800 N: 1.387 → 1.310 passes
