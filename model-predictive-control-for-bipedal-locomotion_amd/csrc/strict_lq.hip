@@ -695,8 +695,9 @@ __global__ void __launch_bounds__(64 * G, 2)
   int klast = -1;      // last pinned slot of this lane's working set (−1: none)
   // diagnostics: clocks of sweep A, sweep B's working-set and tail segments, the rest; task
   // [0] sweep A tail, [1] sweep A working set, [2] sweep B's segment set-up and checkpoint
-  // wait, [4] its Riccati recompute, [5] forward, [6] costate, [7] sweep B tail, [3] the rest
-  unsigned long long pc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  // wait ([9] of segment 1), [4] its Riccati recompute, [5] forward, [6] costate, [7] sweep B
+  // tail, [3] the rest
+  unsigned long long pc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long pt = (kLqProf && a.prof) ? clock64() : 0, ptask = pt;
   auto lap = [&](int ph) {
     if (kLqProf && a.prof) {
@@ -821,9 +822,12 @@ __global__ void __launch_bounds__(64 * G, 2)
             seg_load_runs<S, true, true>(a, j, L, i, rc, fl, cur);
           else
             seg_load<S, true>(a, j, L, i, fl, cur);
-          if (kLqProf && a.prof) {  // (diagnostics: the checkpoint's arrival timed apart)
-            __builtin_amdgcn_s_waitcnt(0);
-            lap(2);
+          if (kLqProf && a.prof) {  // (diagnostics: the checkpoint's arrival timed apart;
+            __builtin_amdgcn_s_waitcnt(0);  // segment 1's, behind sweep A's stores, separately)
+            if (j == 1)
+              lap(9);
+            else
+              lap(2);
           }
           auto nx = [&](Ric& w) { next(w, j); };
 #ifdef ZMPC_DIAG
@@ -928,8 +932,8 @@ __global__ void __launch_bounds__(64 * G, 2)
     pc[8] = clock64() - ptask;
     if (lane == 0) {
 #pragma unroll
-      for (int q = 0; q < 9; ++q) atomicAdd(a.prof + axis * 10 + q, pc[q]);
-      atomicAdd(a.prof + axis * 10 + 9, 1ull);
+      for (int q = 0; q < 10; ++q) atomicAdd(a.prof + axis * 11 + q, pc[q]);
+      atomicAdd(a.prof + axis * 11 + 10, 1ull);
     }
   }
   if (valid && a.status != nullptr) {
@@ -1199,11 +1203,11 @@ hipError_t launch_lq(const zmpc_plan* p, LqArgs& a, int64_t waves, hipStream_t s
 #ifdef ZMPC_DIAG
   static unsigned long long* prof = [] {  // diagnostics build: per-phase clocks to stderr
     unsigned long long* q = nullptr;
-    if (getenv("ZMPC_LQ_PROF") && hipMalloc((void**)&q, 20 * sizeof(unsigned long long)) != hipSuccess)
+    if (getenv("ZMPC_LQ_PROF") && hipMalloc((void**)&q, 22 * sizeof(unsigned long long)) != hipSuccess)
       q = nullptr;
     return q;
   }();
-  if (prof) (void)hipMemsetAsync(prof, 0, 20 * sizeof(unsigned long long), s);
+  if (prof) (void)hipMemsetAsync(prof, 0, 22 * sizeof(unsigned long long), s);
   a.prof = prof;
 #else
   a.prof = nullptr;
@@ -1212,17 +1216,17 @@ hipError_t launch_lq(const zmpc_plan* p, LqArgs& a, int64_t waves, hipStream_t s
                      (const double*)p->lqtab);
   hipError_t e = hipGetLastError();
   if (a.prof && e == hipSuccess) {
-    unsigned long long h[20];
+    unsigned long long h[22];
     (void)hipMemcpy(h, a.prof, sizeof(h), hipMemcpyDeviceToHost);
     for (int ax = 0; ax < 2; ++ax) {
-      const unsigned long long* c = h + 10 * ax;
-      const double t = (double)(c[8] ? c[8] : 1), nt = (double)(c[9] ? c[9] : 1);
+      const unsigned long long* c = h + 11 * ax;
+      const double t = (double)(c[8] ? c[8] : 1), nt = (double)(c[10] ? c[10] : 1);
       fprintf(stderr,
               "lq prof axis %d: %llu tasks, %.0f clocks/task: sweep A tail %.3f, sweep A "
-              "working-set %.3f; sweep B working-set: set-up + checkpoint wait %.3f, Riccati "
-              "%.3f, forward %.3f, costate %.3f; sweep B tail %.3f; rest %.3f\n",
-              ax, c[9], t / nt, c[0] / t, c[1] / t, c[2] / t, c[4] / t, c[5] / t, c[6] / t,
-              c[7] / t, c[3] / t);
+              "working-set %.3f; sweep B working-set: set-up + checkpoint wait %.3f (segment 1 "
+              "%.3f), Riccati %.3f, forward %.3f, costate %.3f; sweep B tail %.3f; rest %.3f\n",
+              ax, c[10], t / nt, c[0] / t, c[1] / t, c[2] / t, c[9] / t, c[4] / t, c[5] / t,
+              c[6] / t, c[7] / t, c[3] / t);
     }
   }
   return e;
