@@ -141,10 +141,10 @@ int zmpc_plan_timings(const zmpc_plan* plan, float* dst_host, int32_t count);
  *                           2 = the reduced-Cholesky one-instance-per-wavefront kernel
  *                           (cross-check), 3 = the LQ kernel, 4 = the parallel-in-time kernel
  *                           (1, 2 and 4: horizons up to 512)
- *   ZMPC_OPT_STRICT_BOUNDS  strict rollouts on the LQ kernel: 0 = auto (run-length for per-walk
- *                           bounds, rows for a shared CoP), 1 = the bounds staged one row per
- *                           sample, 2 = run-length bounds (one entry per run of equal bounds);
- *                           bitwise the same results
+ *   ZMPC_OPT_STRICT_BOUNDS  strict rollouts on the LQ kernel: 0 = auto (run-length bounds;
+ *                           rows for a shared CoP before round 5), 1 = the bounds staged one row
+ *                           per sample, 2 = run-length bounds (one entry per run of equal
+ *                           bounds); bitwise the same results
  * Returns ZMPC_EINVAL for an unknown option or value.
  */
 #define ZMPC_OPT_CORRELATION 0

@@ -1168,8 +1168,10 @@ hipError_t launch_lq(const zmpc_plan* p, LqArgs& a, int64_t waves, hipStream_t s
   if (!var) return hipErrorInvalidValue;
   const int64_t blocks = (waves + var->G - 1) / var->G;
   const size_t lds = lq_lds_bytes(var->G, p->N);
-  // rollouts over per-walk bounds: non-temporal checkpoints (see CkIO)
-  bool nt = !a.window_mode && !a.shared;
+  // cached checkpoints (see CkIO: with run-length bounds the window rows no longer compete
+  // for the caches, and non-temporal checkpoints became the slower form — config 3 55.4 vs
+  // 56.7 ms, diagnostics build, profiles/r5/r5m/)
+  bool nt = false;
 #ifdef ZMPC_DIAG
   if (const char* e = getenv("ZMPC_LQ_NT")) nt = atoi(e) != 0;  // (diagnostics: A/B of the policy)
 #endif
@@ -1291,11 +1293,13 @@ hipError_t zmpc_launch_rollout_strict_lq(const zmpc_plan* p, int64_t B, int64_t 
   const int64_t G = var->G;  // checkpoints for every wave of the launched blocks
   const size_t ck_doubles = (size_t)((waves + G - 1) / G * G) * a.NS * kCkStride;
   // bounds: rows (2 axes × rows × 64 (z_ref, half-width)) or runs (per (axis, group) up to
-  // n + 2 runs of a pair and a start time).  ZMPC_OPT_STRICT_BOUNDS 0 (auto): runs for per-walk
-  // bounds, rows for a shared CoP (profiles/r4/r4e_*: config 3 71.8 → 64.3 ms with runs, L2
-  // fetch 122 → 24 GB per launch; config 4's shared rows stay in L2: 80.5 ms rows, 87.1 runs)
+  // n + 2 runs of a pair and a start time).  ZMPC_OPT_STRICT_BOUNDS 0 (auto) = runs
+  // (profiles/r4/r4e_*: config 3 71.8 → 64.3 ms with runs, L2 fetch 122 → 24 GB per launch).
+  // A shared CoP's rows stay in L2, and round 4 kept rows for it (80.5 ms rows, 87.1 runs);
+  // with the per-segment crossing test the runs are faster there too (config 4 64.0–64.4 vs
+  // 65.5–66.1 ms, profiles/r5/r5l/).
   const int bopt = p->opt[ZMPC_OPT_STRICT_BOUNDS];
-  const bool runs = bopt == 2 || (bopt == 0 && bstride != 0);
+  const bool runs = bopt != 1;
   a.rstride = (n + 2) * 64;
   const size_t st_doubles = runs ? (size_t)2 * a.groups * a.rstride * 3
                                  : (size_t)2 * a.groups * a.rows * 64 * 2;
