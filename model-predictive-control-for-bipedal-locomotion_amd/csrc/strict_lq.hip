@@ -1170,7 +1170,7 @@ hipError_t launch_lq(const zmpc_plan* p, LqArgs& a, int64_t waves, hipStream_t s
   const size_t lds = lq_lds_bytes(var->G, p->N);
   // cached checkpoints (see CkIO: with run-length bounds the window rows no longer compete
   // for the caches, and non-temporal checkpoints became the slower form — config 3 55.4 vs
-  // 56.7 ms, diagnostics build, profiles/r5/r5m/)
+  // 56.7 ms, diagnostics build, profiles/r5m/)
   bool nt = false;
 #ifdef ZMPC_DIAG
   if (const char* e = getenv("ZMPC_LQ_NT")) nt = atoi(e) != 0;  // (diagnostics: A/B of the policy)
@@ -1297,7 +1297,7 @@ hipError_t zmpc_launch_rollout_strict_lq(const zmpc_plan* p, int64_t B, int64_t 
   // (profiles/r4/r4e_*: config 3 71.8 → 64.3 ms with runs, L2 fetch 122 → 24 GB per launch).
   // A shared CoP's rows stay in L2, and round 4 kept rows for it (80.5 ms rows, 87.1 runs);
   // with the per-segment crossing test the runs are faster there too (config 4 64.0–64.4 vs
-  // 65.5–66.1 ms, profiles/r5/r5l/).
+  // 65.5–66.1 ms, profiles/r5l/).
   const int bopt = p->opt[ZMPC_OPT_STRICT_BOUNDS];
   const bool runs = bopt != 1;
   a.rstride = (n + 2) * 64;
