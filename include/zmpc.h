@@ -134,7 +134,7 @@ int zmpc_plan_timings(const zmpc_plan* plan, float* dst_host, int32_t count);
  *                           one-wave-per-walk kernel (the cross-check of the split kernels)
  *   ZMPC_OPT_KICK_ORDER     strict rollouts: 1 = walks mapped to lanes in (kick step, kick)
  *                           order (default), 0 = input order
- *   ZMPC_OPT_STRICT_SOLVER  strict plans: 0 = auto (small batches — up to 24576 (walk, axis)
+ *   ZMPC_OPT_STRICT_SOLVER  strict plans: 0 = auto (small batches — up to 16384 (walk, axis)
  *                           instances — the parallel-in-time one-instance-per-wavefront kernel,
  *                           larger ones the LQ lane-per-instance kernel), 1 = the reduced-
  *                           Cholesky tile kernel (16 instances per workgroup; cross-check),

@@ -1051,8 +1051,10 @@ static hipError_t launch_strict(const zmpc_plan* p, StrictArgs a, hipStream_t s,
 // Option 4 / auto at up to kScanMaxInst instances: the parallel-in-time kernel of
 // strict_scan.hip (one instance per wave, the horizon over the lanes).  Crossover measured at
 // N = 150, n = 420 (profiles/r4/r4h_crossover.jsonl): 4096 walks 19.9 vs 55.2 ms (LQ), 8192
-// walks 35.6 vs 56.8, 16384 walks 65.2 vs 57.8 — the LQ kernel wins from ≈14 000 walks.
-constexpr int64_t kScanMaxInst = 24576;
+// walks 35.6 vs 56.8, 16384 walks 65.2 vs 57.8 — the LQ kernel won from ≈14 000 walks.  Round 5
+// (profiles/r5r/cross.jsonl; both kernels faster): 8192 walks 45.0 vs 47.0 ms, 12288 walks 64.9
+// vs 47.6 — the LQ kernel wins from ≈8 600 walks.
+constexpr int64_t kScanMaxInst = 16384;
 enum { kTile = 1, kWave = 2, kLq = 3, kScan = 4 };
 
 static int strict_mode(const zmpc_plan* p, int64_t ninst) {

@@ -285,7 +285,11 @@ __device__ __forceinline__ void shfl_down_elem(const Elem& e, Elem& o, int d) {
 // has converged keeps its working set while the others of its wave iterate (a converged set
 // reproduces itself, so its extra passes change nothing; they are not counted).
 template <int C, int L>
-__global__ void __launch_bounds__(64, (C >= 4 ? 1 : 2)) zmpc_strict_scan_kernel(ScanArgs a) {
+#ifndef ZMPC_SCAN_ONE_WAVE_C  // (chunk widths from which a SIMD holds one wave: A/B builds)
+#define ZMPC_SCAN_ONE_WAVE_C 3
+#endif
+__global__ void __launch_bounds__(64, (C >= ZMPC_SCAN_ONE_WAVE_C ? 1 : 2))
+    zmpc_strict_scan_kernel(ScanArgs a) {
   static_assert(L == 64 || L == 32 || L == 16, "lanes per instance");
   const int lane = threadIdx.x;
   const int il = lane & (L - 1);     // lane within the instance
@@ -615,9 +619,11 @@ void fill(const zmpc_plan* p, ScanArgs& a) {
 
 // Lanes per instance: a whole wave while the instances fit the chip's resident waves (the
 // latency of one pass is what counts), 32 beyond (half the waves; chunks of up to 10 slots,
-// N ≤ 320).  Chunks of C ≥ 4 slots per lane hold 1 wave per SIMD (their state
+// N ≤ 320).  Chunks of C ≥ 3 slots per lane hold 1 wave per SIMD (their state
 // spills past 256 VGPRs into AGPRs instead of scratch: __launch_bounds__ above), shorter ones 2.
-int waves_per_simd(int C) { return C >= 4 ? 1 : 2; }
+// (C = 3 at 2 waves per SIMD spilled 12 B to scratch, and took 64 lanes per instance where one
+// wave per SIMD takes 32: 1024 walks at N = 150 10.2 → 6.2 ms, profiles/r5q/.)
+int waves_per_simd(int C) { return C >= ZMPC_SCAN_ONE_WAVE_C ? 1 : 2; }
 
 int lanes_per_instance(const zmpc_plan* p, int64_t ninst) {
   const int64_t cus = p->cus > 0 ? p->cus : 256;

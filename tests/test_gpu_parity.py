@@ -985,10 +985,10 @@ def test_strict_weights_drop_in(w):
     assert rmse(y_hist[:, :, 0] @ c.C, d[f"w{w}_n150_yhist"] @ c.C) <= 1e-9
 
 
-@pytest.mark.parametrize("B,auto", ((2, 4), (300, 4), (2100, 4), (12300, 3)))
+@pytest.mark.parametrize("B,auto", ((2, 4), (300, 4), (2100, 4), (8192, 4), (8200, 3)))
 def test_strict_small_and_large_batch_paths_agree(B, auto):
     """The automatic choice (ZMPC_OPT_STRICT_SOLVER = 0) takes the parallel-in-time kernel up to
-    24576 instances (whole waves per instance up to the resident waves, 32 lanes beyond) and the
+    16384 instances (whole waves per instance up to the resident waves, 32 lanes beyond) and the
     LQ kernel beyond; on config-3 style batches the small-batch kernels
     (forced) and the LQ kernel give the same histories to rounding, and the automatic one equals
     the chosen kernel's bitwise."""
