@@ -253,7 +253,8 @@ int zmpc_plan_set_option(zmpc_plan* P, int32_t option, int64_t value) {
     return fail(ZMPC_EINVAL, "the small-batch and reduced-Cholesky strict kernels need a strict "
                              "plan, N <= 512");
   if (option == ZMPC_OPT_STRICT_SOLVER && value == 3 && !zmpc_strict_lq_supported(P))
-    return fail(ZMPC_EINVAL, "the LQ strict kernel needs a strict plan, N <= 2560");
+    return fail(ZMPC_EINVAL, "the LQ strict kernel needs a strict plan, N <= " +
+                                  std::to_string(ZMPC_STRICT_MAX_N));
   P->opt[option] = (int)value;
   return ZMPC_OK;
 }

@@ -1132,21 +1132,23 @@ struct LqVariant {
 #define ZMPC_LQV(G) {G, ZMPC_LQK(G, false), nullptr, nullptr, nullptr, nullptr}
 const LqVariant kLqVariants[] = {
     {8, ZMPC_LQK(8, false), ZMPC_LQK(8, true)},  // default
-    ZMPC_LQV(4),  // N up to 640
-    ZMPC_LQV(2),  // N up to 1280
-    ZMPC_LQV(1),  // N up to 2560
+    ZMPC_LQV(4),  // N up to 544 (the default G = 8: up to 224)
+    ZMPC_LQV(2),  // N up to 1184
+    ZMPC_LQV(1),  // N up to 2464
 };
 #undef ZMPC_LQV
 #undef ZMPC_LQK
 constexpr size_t kLdsCap = 160 * 1024;
 
 // LDS of one workgroup: the G waves' slot flags, parked V and state ([12][64] doubles each).
-size_t lq_lds_bytes(int G, int N) {
+constexpr size_t lq_lds_bytes(int G, int N) {
   const size_t rows = (size_t)(N + LQ_S - 1) / LQ_S * LQ_S;
   return (size_t)G * (rows * 64 + 12 * 64 * sizeof(double));
 }
 
-// The largest workgroup whose slot flags fit a CU (N ≤ 2560 at G = 1).
+static_assert(lq_lds_bytes(1, ZMPC_STRICT_MAX_N) <= kLdsCap, "ZMPC_STRICT_MAX_N past the LDS");
+
+// The largest workgroup whose slot flags and parks fit a CU (N ≤ 2464 at G = 1).
 const LqVariant* lq_variant_for(int N) {
   for (const LqVariant& c : kLqVariants)
     if (lq_lds_bytes(c.G, N) <= kLdsCap) return &c;

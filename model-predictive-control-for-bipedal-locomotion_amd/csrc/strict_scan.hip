@@ -617,18 +617,17 @@ void fill(const zmpc_plan* p, ScanArgs& a) {
   a.cnt = p->lqcnt;
 }
 
-// Lanes per instance: a whole wave while the instances fit the chip's resident waves (the
-// latency of one pass is what counts), 32 beyond (half the waves; chunks of up to 10 slots,
-// N ≤ 320).  Chunks of C ≥ 3 slots per lane hold 1 wave per SIMD (their state
-// spills past 256 VGPRs into AGPRs instead of scratch: __launch_bounds__ above), shorter ones 2.
-// (C = 3 at 2 waves per SIMD spilled 12 B to scratch, and took 64 lanes per instance where one
-// wave per SIMD takes 32: 1024 walks at N = 150 10.2 → 6.2 ms, profiles/r5q/.)
-int waves_per_simd(int C) { return C >= ZMPC_SCAN_ONE_WAVE_C ? 1 : 2; }
-
+// Lanes per instance: a whole wave while the instances fit one wave per SIMD (the latency of
+// one pass is what counts), 32 beyond (two instances per wave; chunks of up to 10 slots,
+// N ≤ 320).  Chunks of C ≥ 3 slots per lane hold 1 wave per SIMD (their state spills past 256
+// VGPRs into AGPRs instead of scratch: __launch_bounds__ above), shorter ones 2.  (C = 3 at 2
+// waves per SIMD spilled 12 B to scratch; 1024 walks at N = 150, 32 lanes at one wave per
+// SIMD: 10.2 → 6.2 ms, profiles/r5q/.)
 int lanes_per_instance(const zmpc_plan* p, int64_t ninst) {
   const int64_t cus = p->cus > 0 ? p->cus : 256;
-  const int64_t resident = cus * 4 * waves_per_simd((p->N + 63) / 64);
-  return (ninst > resident && p->N <= 320) ? 32 : 64;
+  // (one instance per SIMD: at N ≤ 128 the whole-wave instances would fit two waves per SIMD,
+  // but two instances per wave already run 1.6–1.8× faster there, profiles/r5t/)
+  return (ninst > cus * 4 && p->N <= 320) ? 32 : 64;
 }
 
 hipError_t launch(const zmpc_plan* p, const ScanArgs& a, hipStream_t s, int L) {

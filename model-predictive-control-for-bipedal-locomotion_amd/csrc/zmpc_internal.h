@@ -22,9 +22,11 @@ constexpr int kScanPowOff = 8 * kScanStride;
 constexpr int kScanGOff = kScanPowOff + 8 * 33 * 9;
 constexpr int kScanDoubles = kScanGOff + 8 * 6;
 
-// Longest strict horizon: the LQ kernel's per-wave slot flags ([N][64] bytes) must fit a CU's
-// LDS for one wave per workgroup (strict_lq.hip lq_variant_for).
-constexpr int ZMPC_STRICT_MAX_N = 2560;
+// Longest strict horizon: the LQ kernel's per-wave LDS — slot flags ([N][64] bytes) and the
+// parked V and state (6 KiB, round 5) — must fit a CU for one wave per workgroup
+// (strict_lq.hip lq_variant_for, checked there by a static_assert): N ≤ 2464 (2560 before the
+// parking).
+constexpr int ZMPC_STRICT_MAX_N = 2464;
 
 struct LipmConsts {
   double T;     // A[0,1] = A[1,2] = B[2]

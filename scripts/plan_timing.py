@@ -16,7 +16,7 @@ torch.cuda.init()
 Plan(0, 150, 0.01, 0.75, 9.81, 1.0, 1e-6, True)  # warm the module / first-launch costs
 for N in Ns:
     for strict in (False, True):
-        if strict and N > 2560:
+        if strict and N > 2464:
             continue
         t0 = time.perf_counter()
         p = Plan(0, N, 1.5 / N, 0.75, 9.81, 1.0, 1e-6, strict)

@@ -894,7 +894,7 @@ def test_strict_long_horizon_step_vs_oracle(N):
 
 def test_strict_horizon_limit():
     with pytest.raises(ValueError, match="strict horizon"):
-        plan(2561, strict=True)
+        plan(2465, strict=True)
 
 
 @pytest.mark.parametrize("solver", (1, 2, 3, 4))
@@ -988,7 +988,7 @@ def test_strict_weights_drop_in(w):
 @pytest.mark.parametrize("B,auto", ((2, 4), (300, 4), (2100, 4), (8192, 4), (8200, 3)))
 def test_strict_small_and_large_batch_paths_agree(B, auto):
     """The automatic choice (ZMPC_OPT_STRICT_SOLVER = 0) takes the parallel-in-time kernel up to
-    16384 instances (whole waves per instance up to the resident waves, 32 lanes beyond) and the
+    16384 instances (whole waves per instance up to one per SIMD, 32 lanes beyond) and the
     LQ kernel beyond; on config-3 style batches the small-batch kernels
     (forced) and the LQ kernel give the same histories to rounding, and the automatic one equals
     the chosen kernel's bitwise."""
@@ -1007,13 +1007,13 @@ def test_strict_small_and_large_batch_paths_agree(B, auto):
         assert rmse(outs[sv][..., 0], outs[3][..., 0]) <= 1e-12, sv
 
 
-@pytest.mark.parametrize("N,B", ((1, 3), (2, 5), (63, 7), (65, 7), (129, 1100), (257, 5),
-                                 (300, 600), (512, 3)))
+@pytest.mark.parametrize("N,B", ((1, 3), (2, 5), (63, 7), (65, 7), (20, 600), (40, 600),
+                                 (129, 1100), (257, 5), (300, 600), (512, 3)))
 def test_strict_scan_kernel_chunk_widths(N, B):
     """The parallel-in-time kernel at the edges of its chunk widths (C = ⌈N/64⌉ = 1..8 slots
     per lane; N = 65/129 leave the last lane one slot, N = 1 a single lane) and with 32 lanes per
-    instance (B = 1100 walks: 2200 instances beyond the resident waves; N = 300, B = 600: 10 slots
-    per lane of 32, one wave per SIMD) against the LQ kernel on
+    instance (beyond one instance per SIMD: B = 600 walks at N = 20 / 40, 1 and 2 slots per lane
+    of 32; B = 1100 at N = 129; N = 300, B = 600: 10 slots per lane of 32) against the LQ kernel on
     the same kicked walks: CoM within 1e-9, same statuses; and one window-mode step."""
     zmax, zmin, x0, F, dt = synthetic_batch(B, 64 if N < 150 else 150, seed=N)
     n = zmax.shape[1]

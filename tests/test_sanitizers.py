@@ -5,7 +5,9 @@ equal the reference's CoM:
 * oracle/strict_lq_cpu.c — the LQ kernel's algorithm in C (the checker and the CPU baseline),
   OpenMP over the walks (tests/san/strict_cpu_main.c drives it);
 * csrc/strict_scan.hip's kernel source on tests/emu's host emulation of the wave (the
-  parallel-in-time kernel's indexing, scans and shuffles).
+  parallel-in-time kernel's indexing, scans and shuffles);
+* csrc/strict_lq.hip's kernel source on the same emulation (the LQ kernel's segments,
+  checkpoints, LDS parking, run cursor and packed flag words).
 GPU code has no sanitizer on this pool; these are the CPU builds of the same code paths."""
 import os
 import shutil
