@@ -135,7 +135,9 @@ struct SegIn {  // a segment's window slots: z_ref, half-width of the box, worki
 template <int S>
 struct SegOut {  // a segment's feedback (v = −K η − kff) and forward outputs, per step
   double K0[S], K1[S], K2[S], kf[S];
-  double w[S];  // forward: v_k (= T³u_k)
+  double w[S];             // forward: v_k (= T³u_k)
+  unsigned long long fw;   // the segment's new flag word (S = 8): the forward's verdicts on the
+                           // free slots, the costate's on the pinned ones; one LDS write
 };
 
 // A free-tail step: P, K, Qux and 1/Quu come from the table, only s moves (strict_eta.h's
@@ -168,6 +170,10 @@ struct RunCursor {
   int ci;      // current run
   int e1, e2;  // forward: starts of runs ci+1, ci+2; backward: starts of runs ci, ci−1
   double r, h, nr, nh;
+  // the neighbour as last loaded: a crossing loads the new run's neighbour here, and the next
+  // segment takes it into (nr, nh, e2) — one segment after the load was issued
+  double pnr, pnh;
+  int pe2;
 };
 
 __device__ __forceinline__ RunCursor run_fwd(const Lane& L, int ci) {
@@ -180,6 +186,9 @@ __device__ __forceinline__ RunCursor run_fwd(const Lane& L, int ci) {
   c.nh = w.y;
   c.e1 = L.rt[(ci + 1) * 64 + L.col];
   c.e2 = L.rt[(ci + 2) * 64 + L.col];
+  c.pnr = c.nr;
+  c.pnh = c.nh;
+  c.pe2 = c.e2;
   return c;
 }
 
@@ -194,16 +203,29 @@ __device__ __forceinline__ RunCursor run_bwd(const Lane& L, int ci) {
   c.nh = w.y;
   c.e1 = L.rt[ci * 64 + L.col];
   c.e2 = L.rt[pi * 64 + L.col];
+  c.pnr = c.nr;
+  c.pnh = c.nh;
+  c.pe2 = c.e2;
   return c;
 }
 
 // Fill a segment's bounds from the runs (times t0 .. t0 + S − 1; backward sweeps descending).
+// Most segments lie inside one run for every lane of the wave: one test per segment.  Where a
+// lane crosses once, the wave walks the slots taking the neighbour already in registers; the
+// crossing lanes load their new run's neighbour into (pnr, pnh, pe2), which nothing reads before
+// the next segment, so the load lands while this segment computes.  (A refill into the cursor
+// itself was read again within the segment: the compiler waited for it at the branch's join —
+// the full latency at every crossing, and in sweep A behind the segment's checkpoint stores.)  A
+// segment in which some lane crosses twice (a run shorter than S slots) takes the per-slot walk
+// with synchronous refills.
 template <int S, bool FWD>
 __device__ __forceinline__ void seg_runs(const Lane& L, int t0, RunCursor& c, double* r,
                                          double* h) {
-  // most segments lie inside one run for every lane: one test per segment, and the per-slot
-  // crossing branches (with their exec-mask bookkeeping) only where a lane crosses
-  if (FWD ? (t0 + S - 1 < c.e1) : (t0 >= c.e1)) {
+  c.nr = c.pnr;
+  c.nh = c.pnh;
+  c.e2 = c.pe2;
+  const bool cross = FWD ? (t0 + S - 1 >= c.e1) : (t0 < c.e1);
+  if (!__any(cross)) {
 #pragma unroll
     for (int q = 0; q < S; ++q) {
       r[q] = c.r;
@@ -211,38 +233,86 @@ __device__ __forceinline__ void seg_runs(const Lane& L, int t0, RunCursor& c, do
     }
     return;
   }
+  const bool twice = FWD ? (t0 + S - 1 >= c.e2) : (t0 < c.e2);
+  if (__any(twice)) {
+    if constexpr (FWD) {
+#pragma unroll
+      for (int q = 0; q < S; ++q) {
+        if (t0 + q >= c.e1) {  // into run ci+1 (runs are ≥ 1 slot: one crossing per slot)
+          ++c.ci;
+          c.r = c.nr;
+          c.h = c.nh;
+          c.e1 = c.e2;
+          const double2 w = L.rs[(c.ci + 1) * 64 + L.col];
+          c.nr = w.x;
+          c.nh = w.y;
+          c.e2 = L.rt[(c.ci + 2) * 64 + L.col];
+        }
+        r[q] = c.r;
+        h[q] = c.h;
+      }
+    } else {
+#pragma unroll
+      for (int q = S - 1; q >= 0; --q) {
+        if (t0 + q < c.e1) {  // into run ci−1
+          --c.ci;
+          c.r = c.nr;
+          c.h = c.nh;
+          c.e1 = c.e2;
+          const int pi = max(c.ci - 1, 0);
+          const double2 w = L.rs[pi * 64 + L.col];
+          c.nr = w.x;
+          c.nh = w.y;
+          c.e2 = L.rt[pi * 64 + L.col];
+        }
+        r[q] = c.r;
+        h[q] = c.h;
+      }
+    }
+    c.pnr = c.nr;
+    c.pnh = c.nh;
+    c.pe2 = c.e2;
+    return;
+  }
+  bool crossed = false;
   if constexpr (FWD) {
 #pragma unroll
     for (int q = 0; q < S; ++q) {
-      if (t0 + q >= c.e1) {  // into run ci+1 (runs are ≥ 1 slot: one crossing per slot)
+      if (t0 + q >= c.e1) {
         ++c.ci;
         c.r = c.nr;
         c.h = c.nh;
         c.e1 = c.e2;
-        const double2 w = L.rs[(c.ci + 1) * 64 + L.col];
-        c.nr = w.x;
-        c.nh = w.y;
-        c.e2 = L.rt[(c.ci + 2) * 64 + L.col];
+        crossed = true;
       }
       r[q] = c.r;
       h[q] = c.h;
     }
+    if (crossed) {
+      const double2 w = L.rs[(c.ci + 1) * 64 + L.col];
+      c.pnr = w.x;
+      c.pnh = w.y;
+      c.pe2 = L.rt[(c.ci + 2) * 64 + L.col];
+    }
   } else {
 #pragma unroll
     for (int q = S - 1; q >= 0; --q) {
-      if (t0 + q < c.e1) {  // into run ci−1
+      if (t0 + q < c.e1) {
         --c.ci;
         c.r = c.nr;
         c.h = c.nh;
         c.e1 = c.e2;
-        const int pi = max(c.ci - 1, 0);
-        const double2 w = L.rs[pi * 64 + L.col];
-        c.nr = w.x;
-        c.nh = w.y;
-        c.e2 = L.rt[pi * 64 + L.col];
+        crossed = true;
       }
       r[q] = c.r;
       h[q] = c.h;
+    }
+    if (crossed) {
+      const int pi = max(c.ci - 1, 0);
+      const double2 w = L.rs[pi * 64 + L.col];
+      c.pnr = w.x;
+      c.pnh = w.y;
+      c.pe2 = L.rt[pi * 64 + L.col];
     }
   }
 }
@@ -397,6 +467,7 @@ __device__ __forceinline__ void seg_forward(const LqArgs& a, int j, const SegIn<
                                             SegOut<S>& g, double* x, double& u0, bool& changed,
                                             int& kl, const Flags& fl, int lane) {
   const double tol = 1e-13;  // as strict.hip (tolz)
+  g.fw = in.fw;  // (a free slot's byte is 0 until its verdict)
 #pragma unroll
   for (int q = 0; q < S; ++q) {
     const int k = j * S + q;
@@ -408,7 +479,10 @@ __device__ __forceinline__ void seg_forward(const LqArgs& a, int j, const SegIn<
       g.w[q] = u;
       const int nf = (d > ht) ? 1 : ((d < -ht) ? -1 : 0);
       if (in.f(q) == 0) {
-        fl.set(k, lane, nf);
+        if constexpr (S == 8)
+          g.fw |= (unsigned long long)(unsigned char)nf << (8 * q);
+        else
+          fl.set(k, lane, nf);
         changed |= nf != 0;
         kl = nf ? k : kl;  // (slots ascend)
       }
@@ -424,6 +498,7 @@ __device__ __forceinline__ void seg_forward_tail(const LqArgs& a, const double* 
                                                  double* x, double& u0, bool& changed, int& kl,
                                                  const Flags& fl, int lane) {
   const double tol = 1e-13;
+  unsigned long long fw = 0;  // (every slot of a tail segment is free for the lanes taking part)
 #pragma unroll
   for (int q = 0; q < S; ++q) {
     const int k = j * S + q;
@@ -434,11 +509,15 @@ __device__ __forceinline__ void seg_forward_tail(const LqArgs& a, const double* 
       if (k == 0) u0 = u;
       const double d = z - in.r[q], ht = in.h[q] + tol;
       const int nf = (d > ht) ? 1 : ((d < -ht) ? -1 : 0);
-      fl.set(k, lane, nf);
+      if constexpr (S == 8)
+        fw |= (unsigned long long)(unsigned char)nf << (8 * q);
+      else
+        fl.set(k, lane, nf);
       changed |= nf != 0;
       kl = nf ? k : kl;
     }
   }
+  if constexpr (S == 8) fl.set_word(j, lane, fw);  // (slots past N stay 0)
 }
 
 // Costate sweep back through segment j from λ at its end (λ_k = ∇V_k(η_k) = Fᵀλ_{k+1} − επ v_k c̄,
@@ -448,6 +527,7 @@ template <int S, bool FULL>
 __device__ __forceinline__ void seg_costate(const LqArgs& a, int j, const SegIn<S>& in,
                                             const SegOut<S>& g, double* lam, bool& changed,
                                             int& kl, const Flags& fl, int lane) {
+  unsigned long long fw = g.fw;
 #pragma unroll
   for (int q = S - 1; q >= 0; --q) {
     const int k = j * S + q;
@@ -459,7 +539,10 @@ __device__ __forceinline__ void seg_costate(const LqArgs& a, int j, const SegIn<
         // wrong-signed multiplier (ν < 0 at z_max, ν > 0 at z_min): σν < −tol
         const bool rel = sg * nu < -a.tolnu;
         if (f != 0) {
-          fl.set(k, lane, rel ? 0 : f);
+          if constexpr (S == 8)
+            fw &= rel ? ~(0xffull << (8 * q)) : ~0ull;
+          else
+            fl.set(k, lane, rel ? 0 : f);
           changed |= rel;
           kl = (!rel && k > kl) ? k : kl;
         }
@@ -467,6 +550,7 @@ __device__ __forceinline__ void seg_costate(const LqArgs& a, int j, const SegIn<
       costate_step(a, g.w[q], lam);
     }
   }
+  if constexpr (S == 8) fl.set_word(j, lane, fw);
 }
 
 // Sweep B through one working-set segment: Riccati from its checkpoint (in v), forward,
