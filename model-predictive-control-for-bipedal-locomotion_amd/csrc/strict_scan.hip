@@ -618,8 +618,8 @@ void fill(const zmpc_plan* p, ScanArgs& a) {
 }
 
 // Lanes per instance: a whole wave while the instances fit one wave per SIMD (the latency of
-// one pass is what counts), 32 beyond (two instances per wave; chunks of up to 10 slots,
-// N ≤ 320).  Chunks of C ≥ 3 slots per lane hold 1 wave per SIMD (their state spills past 256
+// one pass is what counts), 32 beyond (two instances per wave; chunks of up to 16 slots,
+// N ≤ 512: N = 330–510 at 1024 walks 8.3e7–9.1e7 → 1.26e8–1.40e8 solves/s, profiles/r5aa/).  Chunks of C ≥ 3 slots per lane hold 1 wave per SIMD (their state spills past 256
 // VGPRs into AGPRs instead of scratch: __launch_bounds__ above), shorter ones 2.  (C = 3 at 2
 // waves per SIMD spilled 12 B to scratch; 1024 walks at N = 150, 32 lanes at one wave per
 // SIMD: 10.2 → 6.2 ms, profiles/r5q/.)
@@ -627,7 +627,7 @@ int lanes_per_instance(const zmpc_plan* p, int64_t ninst) {
   const int64_t cus = p->cus > 0 ? p->cus : 256;
   // (one instance per SIMD: at N ≤ 128 the whole-wave instances would fit two waves per SIMD,
   // but two instances per wave already run 1.6–1.8× faster there, profiles/r5t/)
-  return (ninst > cus * 4 && p->N <= 320) ? 32 : 64;
+  return (ninst > cus * 4 && p->N <= 512) ? 32 : 64;
 }
 
 hipError_t launch(const zmpc_plan* p, const ScanArgs& a, hipStream_t s, int L) {
@@ -640,7 +640,8 @@ hipError_t launch(const zmpc_plan* p, const ScanArgs& a, hipStream_t s, int L) {
     hipLaunchKernelGGL((zmpc_strict_scan_kernel<CC, 32>), grid, blk, 0, s, a); \
     break;
       ZMPC_SCASE(1) ZMPC_SCASE(2) ZMPC_SCASE(3) ZMPC_SCASE(4) ZMPC_SCASE(5) ZMPC_SCASE(6)
-      ZMPC_SCASE(7) ZMPC_SCASE(8) ZMPC_SCASE(9) ZMPC_SCASE(10)
+      ZMPC_SCASE(7) ZMPC_SCASE(8) ZMPC_SCASE(9) ZMPC_SCASE(10) ZMPC_SCASE(11) ZMPC_SCASE(12)
+      ZMPC_SCASE(13) ZMPC_SCASE(14) ZMPC_SCASE(15) ZMPC_SCASE(16)
 #undef ZMPC_SCASE
       default:
         return hipErrorInvalidValue;

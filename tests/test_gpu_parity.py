@@ -1008,12 +1008,14 @@ def test_strict_small_and_large_batch_paths_agree(B, auto):
 
 
 @pytest.mark.parametrize("N,B", ((1, 3), (2, 5), (63, 7), (65, 7), (20, 600), (40, 600),
-                                 (129, 1100), (257, 5), (300, 600), (512, 3)))
+                                 (129, 1100), (257, 5), (300, 600), (400, 600), (512, 3),
+                                 (512, 600)))
 def test_strict_scan_kernel_chunk_widths(N, B):
     """The parallel-in-time kernel at the edges of its chunk widths (C = ⌈N/64⌉ = 1..8 slots
     per lane; N = 65/129 leave the last lane one slot, N = 1 a single lane) and with 32 lanes per
     instance (beyond one instance per SIMD: B = 600 walks at N = 20 / 40, 1 and 2 slots per lane
-    of 32; B = 1100 at N = 129; N = 300, B = 600: 10 slots per lane of 32) against the LQ kernel on
+    of 32; B = 1100 at N = 129; B = 600 at N = 300 / 400 / 512: 10 / 13 / 16 slots per lane of
+    32) against the LQ kernel on
     the same kicked walks: CoM within 1e-9, same statuses; and one window-mode step."""
     zmax, zmin, x0, F, dt = synthetic_batch(B, 64 if N < 150 else 150, seed=N)
     n = zmax.shape[1]
