@@ -525,9 +525,9 @@ __device__ __forceinline__ void seg_forward_tail(const LqArgs& a, const double* 
 // new flags (the free slots' were set by the forward); kl = the last slot pinned in the new set.
 template <int S, bool FULL>
 __device__ __forceinline__ void seg_costate(const LqArgs& a, int j, const SegIn<S>& in,
-                                            const SegOut<S>& g, double* lam, bool& changed,
+                                            SegOut<S>& g, double* lam, bool& changed,
                                             int& kl, const Flags& fl, int lane) {
-  unsigned long long fw = g.fw;
+  unsigned long long& fw = g.fw;  // (written to LDS by the caller)
 #pragma unroll
   for (int q = S - 1; q >= 0; --q) {
     const int k = j * S + q;
@@ -550,7 +550,6 @@ __device__ __forceinline__ void seg_costate(const LqArgs& a, int j, const SegIn<
       costate_step(a, g.w[q], lam);
     }
   }
-  if constexpr (S == 8) fl.set_word(j, lane, fw);
 }
 
 // Sweep B through one working-set segment: Riccati from its checkpoint (in v), forward,
@@ -563,7 +562,7 @@ template <int S, bool FULL, bool RECOMP, class Next, class Lap>
 __device__ __forceinline__ void seg_sweep_b(const LqArgs& a, int j, Ric& v, const SegIn<S>& in,
                                             SegOut<S>& g, double* xs, double& u0, bool& changed,
                                             int& kl, const Flags& fl, int lane, double* vpark,
-                                            Next& next, Lap& lap) {
+                                            Next& next, Lap& lap, bool fr) {
   if constexpr (RECOMP) {
     // V at the segment's end, parked in LDS until the costate needs it (its registers hold the
     // next checkpoint meanwhile)
@@ -574,14 +573,19 @@ __device__ __forceinline__ void seg_sweep_b(const LqArgs& a, int j, Ric& v, cons
   lap(4);
   seg_forward<S, FULL>(a, j, in, g, xs, u0, changed, kl, fl, lane);
   lap(5);
-  double lam[3];
-  {
-    const double* q = vpark + lane;
-    lam[0] = fma(q[0], xs[0], fma(q[64], xs[1], q[128] * xs[2])) - q[384];
-    lam[1] = fma(q[64], xs[0], fma(q[192], xs[1], q[256] * xs[2])) - q[448];
-    lam[2] = fma(q[128], xs[0], fma(q[256], xs[1], q[320] * xs[2])) - q[512];
+  // (a segment no lane taking part pins needs no costate: it only prices pinned slots, and
+  // the next segment's λ comes from its own parked V)
+  if (!fr) {
+    double lam[3];
+    {
+      const double* q = vpark + lane;
+      lam[0] = fma(q[0], xs[0], fma(q[64], xs[1], q[128] * xs[2])) - q[384];
+      lam[1] = fma(q[64], xs[0], fma(q[192], xs[1], q[256] * xs[2])) - q[448];
+      lam[2] = fma(q[128], xs[0], fma(q[256], xs[1], q[320] * xs[2])) - q[512];
+    }
+    seg_costate<S, FULL>(a, j, in, g, lam, changed, kl, fl, lane);
   }
-  seg_costate<S, FULL>(a, j, in, g, lam, changed, kl, fl, lane);
+  if constexpr (S == 8) fl.set_word(j, lane, g.fw);
   lap(6);
 }
 
@@ -919,15 +923,16 @@ __global__ void __launch_bounds__(64 * G, 2)
           if (seg_free(cur)) ++n_sb_free;
 #endif
           // (43 % of these segments have no pinned slot in any lane taking part, config 3,
-          // diagnostics build; a free form for them — ric_free, forward, primal verdicts, no
-          // costate — spills at 256 VGPRs: 74.9 vs 65.0 ms, and 66.7 ms at S = 6,
-          // profiles/r4/r4n/)
+          // diagnostics build: they skip the costate — config 3 51.3 → 50.0 ms, profiles/r5ae/.
+          // A free Riccati form for them as well spills: 300 B in round 5, and 74.9 vs 65.0 ms
+          // in round 4, profiles/r4/r4n/)
+          const bool fr = seg_free(cur);
           if (j < jfull) {
             seg_sweep_b<S, true, decltype(R)::value>(a, j, v, cur, g, xs, u0, changed, kl, fl,
-                                                     lane, vpark, nx, lap);
+                                                     lane, vpark, nx, lap, fr);
           } else {
             seg_sweep_b<S, false, decltype(R)::value>(a, j, v, cur, g, xs, u0, changed, kl, fl,
-                                                      lane, vpark, nx, lap);
+                                                      lane, vpark, nx, lap, fr);
           }
         };
         if (jt > 0) seg_b(0, std::false_type{});  // (sweep A's feedback)
