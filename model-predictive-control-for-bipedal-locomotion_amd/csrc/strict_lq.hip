@@ -719,6 +719,16 @@ __global__ void __launch_bounds__(64 * G, 2)
   // bounds follow the positions (table (axis, pos / 64), column pos % 64), everything per walk
   // (x0, kick, history, status) b
   const bool valid = pos < a.B;
+  // one resident round (no queue): the y waves carry nearly all the working-set work and set
+  // the kernel's time, so they issue first when their SIMD's x wave competes (wave priority;
+  // the x waves take the slack) — config 3 50.0 → 45.5 ms.  With the queue the same priority
+  // cost config 4 62.7 → 65.0 ms (its later rounds mix y and x tasks), profiles/r5aj/.
+  if constexpr (!QUEUE) {
+    if (axis == 1)
+      __builtin_amdgcn_s_setprio(2);
+    else
+      __builtin_amdgcn_s_setprio(0);
+  }
   const int64_t b = (valid && a.perm) ? (int64_t)a.perm[pos] : pos;
   Lane L;
   L.lane = lane;

@@ -103,6 +103,7 @@ inline int atomicAdd(int* p, int v) {
 inline int __builtin_amdgcn_readfirstlane(int v) { return v; }
 inline void __builtin_amdgcn_sched_barrier(int) {}
 inline void __builtin_amdgcn_s_waitcnt(int) {}
+inline void __builtin_amdgcn_s_setprio(int) {}
 #define __builtin_nontemporal_store(v, p) (*(p) = (v))
 #define __builtin_nontemporal_load(p) (*(p))
 inline unsigned long long clock64() { return 0; }
