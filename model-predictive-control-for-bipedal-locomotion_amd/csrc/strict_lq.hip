@@ -1285,7 +1285,11 @@ hipError_t launch_lq(const zmpc_plan* p, LqArgs& a, int64_t waves, hipStream_t s
   int64_t grid = blocks;
   int* queue = a.queue;
   a.queue = nullptr;
-  if (queue != nullptr && kq != nullptr && !a.window_mode) {
+  bool use_queue = true;
+#ifdef ZMPC_DIAG
+  if (getenv("ZMPC_LQ_NOQUEUE")) use_queue = false;  // (diagnostics: A/B of the queue form)
+#endif
+  if (use_queue && queue != nullptr && kq != nullptr && !a.window_mode) {
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)kq, 64 * var->G, lds) !=
         hipSuccess) {
