@@ -806,6 +806,11 @@ def main():
                     help="also time batches pipelined two-deep on two streams (reported beside "
                          "value; off by default so a profile of the default command sees only "
                          "non-overlapped launches)")
+    ap.add_argument("--strict-steps", type=int, default=3,
+                    help="default line (config 2): timed launches of the config-3 strict "
+                         "sub-record (0 = no sub-record)")
+    ap.add_argument("--strict-cpu-seconds", type=float, default=4.0,
+                    help="CPU-leg budget per process of the strict sub-record")
     ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
                     help="plan option (mpc_bipedal/_native.py OPTIONS, include/zmpc.h "
                          "ZMPC_OPT_*) for A/B timing of forms with the same results")
@@ -856,11 +861,40 @@ def main():
     conf = 3 if args.strict else args.config
     if CONFIGS[conf].get("herdt"):
         line = herdt_bench(args, rank, world, dev, dist_on)
-        if rank == 0:
-            print(json.dumps(line))
-        if dist_on:
-            dist.destroy_process_group()
-        return
+    else:
+        line = rollout_bench(args, conf, rank, world, dev, dist_on)
+        if conf == 2 and args.strict_steps > 0 and not args.batch and not args.horizon:
+            # the strict experiment (run_compare_resistance.py:87-169; default.json:18
+            # "strict": true) beside the headline: config 3 in its own timed region
+            sub = strict_subrecord(args, rank, world, dev, dist_on)
+            if rank == 0:
+                line["strict"] = sub
+    if rank == 0:
+        print(json.dumps(line))
+    if dist_on:
+        dist.destroy_process_group()
+
+
+def strict_subrecord(args, rank, world, dev, dist_on):
+    """Config 3 (B = 65 536 walks per GPU, N = 150, strict, f64) as a sub-record of the default
+    line: its own warm-up and timed region (barrier + synchronize on both sides, max over
+    ranks), roofline (counted FP64 work, algorithmic bytes, PMC traffic) and, at one GPU, the
+    CPU legs with a shorter budget.  The headline `value` stays config 2's."""
+    sa = argparse.Namespace(**vars(args))
+    sa.steps, sa.warmup = args.strict_steps, 1
+    sa.batch, sa.horizon, sa.option = None, None, []
+    sa.unconstrained, sa.pipelined, sa.no_dense_leg = False, False, True
+    sa.cpu_seconds = args.strict_cpu_seconds
+    sub = rollout_bench(sa, 3, rank, world, dev, dist_on)
+    if rank != 0:
+        return None
+    for k in ("metric", "higher_is_better", "vs_baseline", "correlation", "pipelined"):
+        sub.pop(k, None)
+    return sub
+
+
+def rollout_bench(args, conf, rank, world, dev, dist_on):
+    """Configs 2-5 (the rollout workloads): the JSON line (rank 0) or None."""
     wl = dict(CONFIGS[conf])
     if args.unconstrained:
         wl["strict"] = False
@@ -922,7 +956,12 @@ def main():
     if rank == 0 and cfg.horizon == 150:
         fx = np.load(os.path.join(ROOT, "tests", "golden", "walk_n150.npz"))
         ref_com = fx["com_force"]
-        if not cfg.strict and ref_com.shape[0] == n:
+        if cfg.strict and not wl["shared"]:
+            # walk 0 = the default walk at F_ext = 400 N: the reference's own strict branch run
+            # with the recording cvxpy stand-in (tests/golden/make_strict_ref_golden.py)
+            ref_com = np.load(os.path.join(ROOT, "tests", "golden", "strict_ref.npz"))[
+                "n150_F400_com"]
+        if ref_com.shape[0] == n:
             com_rmse_ref = float(np.sqrt(np.mean(
                 (hist[0, :, :, 0].cpu().numpy() - ref_com) ** 2)))
 
@@ -1087,9 +1126,10 @@ def main():
             "correlation": corr,
             "plan": plan_rec,
         }
-        print(json.dumps(line))
-    if dist_on:
-        dist.destroy_process_group()
+        plan.destroy()
+        return line
+    plan.destroy()
+    return None
 
 
 if __name__ == "__main__":

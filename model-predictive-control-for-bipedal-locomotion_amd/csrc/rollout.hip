@@ -25,7 +25,9 @@
 #include <algorithm>
 #include <climits>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
+#include <vector>
 
 #include "zmpc_internal.h"
 
@@ -221,6 +223,7 @@ struct RolloutArgs {
   int hN;                 // horizon N (ksum layout)
   int64_t pf_ahead;       // one walk per workgroup: touch walk b + pf_ahead's bounds (the next
                           // dispatch round's) into the caches early; 0 = off
+  unsigned long long* tl;  // diagnostics build only (ZMPC_ROLLOUT_TL): per-walk phase stamps
 };
 
 // Diagnostic ablation bits (ZMPC_DEBUG_ROLLOUT: 1 no correlation, 2 no scan, 4 no history
@@ -228,8 +231,14 @@ struct RolloutArgs {
 // -DZMPC_DIAG); the product library has none of them.
 #ifdef ZMPC_DIAG
 __device__ __forceinline__ int dbgb(const RolloutArgs& a, int bit) { return a.dbg & bit; }
+// phase stamps of walk b (wave 0's view, the 100 MHz constant clock): [0] start, [1] bounds in
+// LDS, [2] correlation done, [3] history staged, [4] copy-out issued
+__device__ __forceinline__ void tl_stamp(const RolloutArgs& a, int64_t b, int k) {
+  if (a.tl != nullptr && threadIdx.x == 0) a.tl[b * 5 + k] = (unsigned long long)wall_clock64();
+}
 #else
 __device__ __forceinline__ constexpr int dbgb(const RolloutArgs&, int) { return 0; }
+__device__ __forceinline__ void tl_stamp(const RolloutArgs&, int64_t, int) {}
 #endif
 
 // a 16-byte store with the non-temporal hint (streamed past the caches)
@@ -726,6 +735,7 @@ __device__ __forceinline__ void split_walk(const RolloutArgs& a, int64_t b, doub
   const int n = a.n, nsteps = n - 1;
   double f[CW];
   double pf0 = 0.0, pf1 = 0.0;  // prefetch results (kept alive to the end, never used)
+  tl_stamp(a, b, 0);
   const double* xb = a.x0 + b * 6 + 3 * axis;
   const double xi[3] = {xb[0], xb[1], xb[2]};
   const double kk = (axis == 1 && a.kick != nullptr) ? a.kick[b] : 0.0;
@@ -775,6 +785,7 @@ __device__ __forceinline__ void split_walk(const RolloutArgs& a, int64_t b, doub
       }
     }
     __syncthreads();
+    tl_stamp(a, b, 1);
     // ---- 3. correlation (this wave's axis) -------------------------------------------------
     // sparse z_ref differences (piecewise-constant CoP) first, else the dense forms
     const bool sparse = a.ksum != nullptr && !dbgb(a, 1) &&
@@ -785,6 +796,7 @@ __device__ __forceinline__ void split_walk(const RolloutArgs& a, int64_t b, doub
     else
       axis_correlate<CW>(a, kg, axis ? zr1 : zr0, lane, f);  // k: wave-uniform scalar loads
     __syncthreads();  // z_ref dead: the area becomes the history staging (n rows of 6)
+    tl_stamp(a, b, 2);
   }
   // ---- 4. lane-chunk affine scan -----------------------------------------------------------
   const int64_t kick_step = (axis == 1) ? kick_step_of(a, b) : -1;
@@ -855,6 +867,7 @@ __device__ __forceinline__ void split_walk(const RolloutArgs& a, int64_t b, doub
     if (lane == 0) flag[axis] = bad ? ZMPC_ST_NONFINITE : 0;
   }
   __syncthreads();
+  tl_stamp(a, b, 3);
   // ---- 6. coalesced copy-out ---------------------------------------------------------------
   if (!dbgb(a, 4)) {
     if constexpr (PM) __builtin_amdgcn_s_setprio(3);
@@ -892,6 +905,7 @@ __device__ __forceinline__ void split_walk(const RolloutArgs& a, int64_t b, doub
     }
     if constexpr (PM) __builtin_amdgcn_s_setprio(0);
   }
+  tl_stamp(a, b, 4);
   if (a.status != nullptr && tid == 0) a.status[b] = flag[0] | flag[1];
   if (a.dbg < 0) hist[tid] = pf0 + pf1;  // never (dbg ≥ 0): keeps the prefetch loads
 }
@@ -1723,6 +1737,24 @@ void launch_wide(hipStream_t s, RolloutArgs q, size_t lds, int64_t B, int cus) {
                      lds, s, q);
 }
 
+// The wide kernel's instance for E points per thread.  E = 8 exists only where its transform
+// (P = 8·128·W points of 16 B) fits the 64 KiB LDS ceiling the launcher enforces, i.e. W ≤ 4:
+// an 8-wave E = 8 instance could never launch.
+template <int C, int W>
+void launch_wide_e(int E, hipStream_t s, const RolloutArgs& q, size_t lds, int64_t B, int cus) {
+  if (E == 4) {
+    launch_wide<C, W, 4>(s, q, lds, B, cus);
+    return;
+  }
+  if constexpr (8 * 128 * W * 16 <= 64 * 1024) {
+    if (E == 8) {
+      launch_wide<C, W, 8>(s, q, lds, B, cus);
+      return;
+    }
+  }
+  launch_wide<C, W, 0>(s, q, lds, B, cus);
+}
+
 // Walks of at most 64·8+1 samples (one correlation pass).  The split kernels (a 128-thread
 // workgroup per walk, one wave per axis) when their LDS fits the default 64 KiB ceiling:
 //   shared CoP (f precomputed): zmpc_rollout_unc_splitd_kernel<CW, true>;
@@ -1831,6 +1863,22 @@ hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, con
   // dense-form timing beside the default)
   a.ksum = p->opt[ZMPC_OPT_CORRELATION] == 1 ? nullptr : p->ksum;
   a.hN = p->N;
+#ifdef ZMPC_DIAG
+  // diagnostics: per-walk phase stamps of the split kernel, written to $ZMPC_ROLLOUT_TL after
+  // every launch ([B][5] u64, wall_clock64 ticks)
+  static const char* tl_path = getenv("ZMPC_ROLLOUT_TL");
+  static unsigned long long* tl_buf = nullptr;
+  static int64_t tl_cap = 0;
+  if (tl_path && B > tl_cap) {
+    if (tl_buf) (void)hipFree(tl_buf);
+    tl_buf = nullptr;
+    tl_cap = hipMalloc((void**)&tl_buf, (size_t)B * 5 * 8) == hipSuccess ? B : 0;
+  }
+  if (tl_buf) {
+    (void)hipMemsetAsync(tl_buf, 0, (size_t)B * 5 * 8, s);
+    a.tl = tl_buf;
+  }
+#endif
   const int long_form = p->opt[ZMPC_OPT_LONG_WALK];  // 0 auto, 1 direct, 2 FFT, 3 chunk kernel
   WideGeom wg;
   if (g.passes > 1 && (long_form == 3 || !wide_geom(p->N, n, &wg))) {
@@ -1877,12 +1925,7 @@ hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, con
     switch (wg.w * 16 + wg.cw) {
 #define ZMPC_WCASE(W, C)                                \
   case W * 16 + C:                                      \
-    if (E == 4)                                         \
-      launch_wide<C, W, 4>(s, q, lds_w, B, p->cus);     \
-    else if (E == 8)                                    \
-      launch_wide<C, W, 8>(s, q, lds_w, B, p->cus);     \
-    else                                                \
-      launch_wide<C, W, 0>(s, q, lds_w, B, p->cus);     \
+    launch_wide_e<C, W>(E, s, q, lds_w, B, p->cus);     \
     break;
       ZMPC_WCASE(2, 4) ZMPC_WCASE(2, 5) ZMPC_WCASE(2, 6) ZMPC_WCASE(2, 7) ZMPC_WCASE(2, 8)
       ZMPC_WCASE(4, 5) ZMPC_WCASE(4, 6) ZMPC_WCASE(4, 7) ZMPC_WCASE(4, 8)
@@ -1918,6 +1961,17 @@ hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, con
       return hipErrorInvalidValue;
   }
   hipError_t e = hipGetLastError();
+#ifdef ZMPC_DIAG
+  if (a.tl && e == hipSuccess) {
+    std::vector<unsigned long long> h((size_t)B * 5);
+    (void)hipStreamSynchronize(s);
+    (void)hipMemcpy(h.data(), a.tl, h.size() * 8, hipMemcpyDeviceToHost);
+    if (FILE* f = fopen(tl_path, "wb")) {
+      fwrite(h.data(), 8, h.size(), f);
+      fclose(f);
+    }
+  }
+#endif
   if (fsh) {
     const hipError_t ef = hipFreeAsync(fsh, s);
     if (e == hipSuccess) e = ef;

@@ -63,14 +63,14 @@ constexpr bool kLqProf = true;  // per-phase clocks (ZMPC_LQ_PROF), diagnostics 
 #else
 constexpr bool kLqProf = false;
 #endif
-#ifndef ZMPC_LQ_S  // (A/B builds only: make ab)
-#define ZMPC_LQ_S 8
-#endif
-#ifndef ZMPC_LQ_DRIFT
+#ifndef ZMPC_LQ_DRIFT  // (A/B builds only: make ab)
 #define ZMPC_LQ_DRIFT 4
 #endif
 
-constexpr int LQ_S = ZMPC_LQ_S;  // Riccati steps per checkpoint segment
+// Riccati steps per checkpoint segment.  Fixed at 8: a segment's working-set flags are one
+// 8-byte LDS word (Flags: [slot / 8][64][8]), which the segment loads, the new-flag writes and
+// the warm-start shift all take whole (rounds 1-3 measured S = 6/10/12/16: slower or spilling).
+constexpr int LQ_S = 8;
 constexpr int LQ_DRIFT = ZMPC_LQ_DRIFT;  // timesteps a lane may run ahead of its wave's slowest lane
                               // (round 3, profiles/r3u/, r3drift/: 0/1/2/4/8 → 104.5/94.8/92.5/
                               // 90.9/92.7 ms at config 3 — the bound rows stay a few rows apart)
@@ -125,7 +125,7 @@ struct LqArgs {
 
 template <int S>
 struct SegIn {  // a segment's window slots: z_ref, half-width of the box, working-set flags
-  static_assert(S <= 8, "a segment's flags are one 8-byte word");
+  static_assert(S == 8, "a segment's flags are one 8-byte word of Flags");
   double r[S], h[S];
   unsigned long long fw;  // the flags, one signed byte per slot: 0 free, +1 at z_max = r + h,
                           // −1 at z_min = r − h
@@ -365,19 +365,10 @@ __device__ __forceinline__ void unpark(const double* vp, Ric& v, int lane) {
   v.s2 = q[512];
 }
 
-// A segment's flags as one word (S = 8: segment j is flag word j; a shorter segment gathers
-// its bytes).
+// A segment's flags as one word (segment j is flag word j).
 template <int S>
 __device__ __forceinline__ unsigned long long seg_flags(const Flags& fl, int j, int lane) {
-  if constexpr (S == 8) {
-    return fl.word(j, lane);
-  } else {
-    unsigned long long w = 0;
-#pragma unroll
-    for (int q = 0; q < S; ++q)
-      w |= (unsigned long long)(unsigned char)fl.get(j * S + q, lane) << (8 * q);
-    return w;
-  }
+  return fl.word(j, lane);
 }
 
 // Issue the loads of segment j's slots (bounds, and the flags when FLAGS).  Slots past N read
@@ -479,10 +470,7 @@ __device__ __forceinline__ void seg_forward(const LqArgs& a, int j, const SegIn<
       g.w[q] = u;
       const int nf = (d > ht) ? 1 : ((d < -ht) ? -1 : 0);
       if (in.f(q) == 0) {
-        if constexpr (S == 8)
-          g.fw |= (unsigned long long)(unsigned char)nf << (8 * q);
-        else
-          fl.set(k, lane, nf);
+        g.fw |= (unsigned long long)(unsigned char)nf << (8 * q);
         changed |= nf != 0;
         kl = nf ? k : kl;  // (slots ascend)
       }
@@ -509,15 +497,12 @@ __device__ __forceinline__ void seg_forward_tail(const LqArgs& a, const double* 
       if (k == 0) u0 = u;
       const double d = z - in.r[q], ht = in.h[q] + tol;
       const int nf = (d > ht) ? 1 : ((d < -ht) ? -1 : 0);
-      if constexpr (S == 8)
-        fw |= (unsigned long long)(unsigned char)nf << (8 * q);
-      else
-        fl.set(k, lane, nf);
+      fw |= (unsigned long long)(unsigned char)nf << (8 * q);
       changed |= nf != 0;
       kl = nf ? k : kl;
     }
   }
-  if constexpr (S == 8) fl.set_word(j, lane, fw);  // (slots past N stay 0)
+  fl.set_word(j, lane, fw);  // (slots past N stay 0)
 }
 
 // Costate sweep back through segment j from λ at its end (λ_k = ∇V_k(η_k) = Fᵀλ_{k+1} − επ v_k c̄,
@@ -539,10 +524,7 @@ __device__ __forceinline__ void seg_costate(const LqArgs& a, int j, const SegIn<
         // wrong-signed multiplier (ν < 0 at z_max, ν > 0 at z_min): σν < −tol
         const bool rel = sg * nu < -a.tolnu;
         if (f != 0) {
-          if constexpr (S == 8)
-            fw &= rel ? ~(0xffull << (8 * q)) : ~0ull;
-          else
-            fl.set(k, lane, rel ? 0 : f);
+          fw &= rel ? ~(0xffull << (8 * q)) : ~0ull;
           changed |= rel;
           kl = (!rel && k > kl) ? k : kl;
         }
@@ -585,7 +567,7 @@ __device__ __forceinline__ void seg_sweep_b(const LqArgs& a, int j, Ric& v, cons
     }
     seg_costate<S, FULL>(a, j, in, g, lam, changed, kl, fl, lane);
   }
-  if constexpr (S == 8) fl.set_word(j, lane, g.fw);
+  fl.set_word(j, lane, g.fw);
   lap(6);
 }
 
@@ -691,9 +673,9 @@ __global__ void __launch_bounds__(64 * G, 2)
   double* xpark = vpark + 9 * 64;
   double* ck = a.ck + (size_t)gw * a.NS * kCkStride;
   const CkIO<NT> io{};
-  // (per-lane counts in 32 bits: ≤ 2(n − 1)·64 passes and ·N slots per lane and task group)
-  unsigned long long n_wave_pass = 0;
-  unsigned n_lane_pass = 0, n_ws_slots = 0;
+  // work counters, wave-uniform 64-bit sums (scalar registers): wave passes, lane passes (the
+  // lanes taking part) and their working-set slots
+  unsigned long long n_wave_pass = 0, n_lane_pass = 0, n_ws_slots = 0;
 #ifdef ZMPC_DIAG
   unsigned long long n_sb_ws = 0, n_sb_free = 0;
 #endif
@@ -813,10 +795,13 @@ __global__ void __launch_bounds__(64 * G, 2)
     int kw = part ? klast : -1;
     for (int o = 32; o > 0; o >>= 1) kw = max(kw, __shfl_xor(kw, o));
     const int jt = __builtin_amdgcn_readfirstlane(kw < 0 ? 0 : kw / S + 1);
+    {
+      const unsigned long long np = (unsigned long long)__popcll(__ballot(part));
+      n_lane_pass += np;
+      n_ws_slots += np * (unsigned long long)min(jt * S, N);
+    }
     if (part) {
       lap(3);
-      ++n_lane_pass;
-      n_ws_slots += (unsigned)min(jt * S, N);
       double u0 = 0.0;
       bool changed = false;
       int kl = -1;
@@ -1062,16 +1047,11 @@ __global__ void __launch_bounds__(64 * G, 2)
     run_task(gw);  // one task per wave (the host takes the queue form for 8-wave blocks only)
   }
   if (a.cnt) {
-    unsigned long long lp = n_lane_pass, ws = n_ws_slots;
-    for (int o = 32; o > 0; o >>= 1) {
-      lp += __shfl_xor(lp, o);
-      ws += __shfl_xor(ws, o);
-      itmax = max(itmax, (unsigned)__shfl_xor((int)itmax, o));
-    }
+    for (int o = 32; o > 0; o >>= 1) itmax = max(itmax, (unsigned)__shfl_xor((int)itmax, o));
     if (lane == 0) {
       atomicAdd(a.cnt + 0, n_wave_pass);
-      atomicAdd(a.cnt + 1, lp);
-      atomicAdd(a.cnt + 2, ws);
+      atomicAdd(a.cnt + 1, n_lane_pass);
+      atomicAdd(a.cnt + 2, n_ws_slots);
       if (gw == 0) atomicAdd(a.cnt + 3, 1ull);
 #ifdef ZMPC_DIAG  // (the Herdt counter slots [6], [7], unused by a strict launch)
       atomicAdd(a.cnt + 6, n_sb_ws);

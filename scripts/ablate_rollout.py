@@ -43,7 +43,7 @@ DBG = [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "0,1,15").split(",
 BS = [int(x) for x in (sys.argv[3] if len(sys.argv) > 3 else "1024,4096,16384").split(",")]
 for B in BS:
   for v in VARIANTS:
-    for dbg in (DBG if B == 4096 else (0,)):
+    for dbg in DBG:
         env = dict(env0, ZMPC_DEBUG_ROLLOUT=str(dbg), ZMPC_ROLLOUT_VARIANT=v)
         r = subprocess.run([sys.executable, "-c", CHILD, str(B), "150", "420"], env=env,
                            capture_output=True, text=True, timeout=120)

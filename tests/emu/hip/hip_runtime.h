@@ -79,6 +79,7 @@ inline unsigned long long __ballot(bool b) {
   emu_yield();
   return m;
 }
+inline int __popcll(unsigned long long m) { return __builtin_popcountll(m); }
 inline int atomicOr(int32_t* p, int v) {
   const int o = *p;
   *p |= v;

@@ -264,7 +264,23 @@ def test_herdt_pass_cap_keeps_last_iterate():
         assert np.all(np.isfinite(xn)), k
         if stv & 1:
             capped += 1
-            # the first pass's iterate, not the zero-jerk fallback
+            # the first pass's iterate, not the zero-jerk fallback.  A cold step's first pass
+            # pins no ZMP row and solves the footstep problem exactly, so its iterate is the
+            # optimum of the reference's QP with the swing-polytope rows only (the rows on the
+            # first footstep's (f_x0, f_y0) alone): pinned against the oracle's exact solve
+            side = "left" if int(g("side")) == 0 else "right"
+            Q, p, G, h, Nq, mq = HO.herdt_qp(c.config, g("x"), g("y"), g("v"), float(g("fx")),
+                                             float(g("fy")), int(g("cur")), g("win"), side)
+            n1 = Nq + mq
+            poly = (np.abs(np.delete(G, [Nq, n1 + Nq], axis=1)).sum(axis=1) == 0) if mq else \
+                np.zeros(len(h), bool)
+            u1, _ = HO.herdt_solve(Q, p, G[poly], h[poly], Nq, mq)
+            ex = A @ x[0, 0] + c.B[:, 0] * u1[0]
+            ey = A @ x[0, 1] + c.B[:, 0] * u1[n1]
+            assert np.abs(xn[0] - ex).max() <= 1e-9 * max(1.0, np.abs(ex).max()), k
+            assert np.abs(xn[1] - ey).max() <= 1e-9 * max(1.0, np.abs(ey).max()), k
+            if mq:
+                assert abs(step[0] - u1[Nq]) <= 1e-9 and abs(step[1] - u1[n1 + Nq]) <= 1e-9, k
             assert np.abs(xn[0] - A @ x[0, 0]).max() > 0 or np.abs(xn[1] - A @ x[0, 1]).max() > 0
         else:
             sol = g("sol")
