@@ -109,7 +109,8 @@ struct PolyLds {
 };
 
 // Facet i of side sd: clip its line {a·d = b} by the other half-spaces (one lane per facet).
-__device__ void polytope_segment(const double (*P)[3], int nfac, int i, double* out) {
+__device__ void polytope_segment(const double (*P)[3], int nfac, int i, double& o0, double& o1,
+                                 double& o2, double& o3) {
   const double ax = P[i][0], ay = P[i][1], b = P[i][2];
   const double n2 = ax * ax + ay * ay;
   const double px = ax * b / n2, py = ay * b / n2;  // foot of the line
@@ -129,14 +130,14 @@ __device__ void polytope_segment(const double (*P)[3], int nfac, int i, double* 
     }
   }
   if (!ok || lo > hi || lo < -1e299 || hi > 1e299) {
-    out[0] = __builtin_nan("");
-    out[1] = out[2] = out[3] = 0.0;
+    o0 = __builtin_nan("");
+    o1 = o2 = o3 = 0.0;
     return;
   }
-  out[0] = px + lo * dx;
-  out[1] = py + lo * dy;
-  out[2] = px + hi * dx;
-  out[3] = py + hi * dy;
+  o0 = px + lo * dx;
+  o1 = py + lo * dy;
+  o2 = px + hi * dx;
+  o3 = py + hi * dy;
 }
 
 // Exact minimiser of ½σx(dx − ux)² + ½σy(dy − uy)² over the polygon {d : a_i·d <= b_i}: the
@@ -409,9 +410,14 @@ __global__ void __launch_bounds__(64) zmpc_herdt_kernel(HerdtArgs a) {
     const int nf = sd == 0 ? a.nfl : a.nfr;
     if (i < ZMPC_HERDT_MAX_FACETS) {
       for (int c = 0; c < 3; ++c) pl.h[sd][i][c] = a.poly[sd][i][c];
-      double e[4] = {__builtin_nan(""), 0.0, 0.0, 0.0};
-      if (i < nf) polytope_segment(a.poly[sd], nf, i, e);
-      for (int c = 0; c < 4; ++c) pl.seg[sd][i][c] = e[c];
+      // (four scalars, not an array: the array's two stores on the no-segment path made the
+      // compiler keep it in scratch, 24 B per lane)
+      double e0 = __builtin_nan(""), e1 = 0.0, e2 = 0.0, e3 = 0.0;
+      if (i < nf) polytope_segment(a.poly[sd], nf, i, e0, e1, e2, e3);
+      pl.seg[sd][i][0] = e0;
+      pl.seg[sd][i][1] = e1;
+      pl.seg[sd][i][2] = e2;
+      pl.seg[sd][i][3] = e3;
     }
     __syncthreads();
   }

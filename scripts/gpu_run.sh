@@ -16,6 +16,8 @@
 #                                      ZMPC_DEBUG_ROLLOUT; default.json CoP data), e.g. ablate:0,1,4:4096
 #   py:<name>:<script and args>        a diagnostic script (python) -> <name>.log; DIAG=1 in the
 #                                      step name (pyd:...) loads the diagnostics build
+#   sq:<B>                             SQ instruction / wait counters of the unconstrained rollout
+#                                      (scripts/gpu_rollout_pmc.sh, CoP walks)
 #   res                                register/scratch report of every kernel (host-side, no GPU)
 set -u
 TAG=$1
@@ -83,6 +85,9 @@ PY
       [ $kind = pyd ] && L=(env ZMPC_LIB=$PWD/model-predictive-control-for-bipedal-locomotion_amd/mpc_bipedal/libzmpc_diag.so)
       timeout -k 10 600 "${L[@]}" python -u $args > "$OUT/$name.log" 2>&1
       rc=$?; tail -4 "$OUT/$name.log" | cut -c1-400; step "py $name" $rc ;;
+    sq)
+      bash scripts/gpu_rollout_pmc.sh "$TAG/sq" "$rest" > "$OUT/sq.log" 2>&1
+      rc=$?; tail -3 "$OUT/sq.log"; step sq $rc ;;
     res)
       for f in rollout strict_lq strict_scan herdt; do
         make -s -C model-predictive-control-for-bipedal-locomotion_amd/csrc resources RES=$f

@@ -1,5 +1,6 @@
 """Diagnostic driver for profilers: 20 launches of the config-2-shaped unconstrained rollout
-(B from argv, default 4096) with whatever ZMPC_* env vars the caller set."""
+(B from argv, default 4096; argv[2] "cop" = the bench's default.json CoP walks (default), "rw" =
+random-walk bounds, the dense correlation) with whatever ZMPC_* env vars the caller set."""
 import os
 import sys
 
@@ -14,11 +15,23 @@ B = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
 N, n = 150, 420
 p = Plan(0, N, 1.5 / N, 0.75, 9.81, 1.0, 1e-6, False)
 rng = np.random.default_rng(0)
-zc = np.cumsum(rng.normal(0, 0.01, (B, n, 2)), 1)
-zmax = torch.as_tensor(zc + 0.05, device="cuda")
-zmin = torch.as_tensor(zc - 0.05, device="cuda")
-x0 = torch.zeros((B, 2, 3), dtype=torch.float64, device="cuda")
-L = p.rollout_launcher(zmax, zmin, x0)
+if (sys.argv[2] if len(sys.argv) > 2 else "cop") == "cop":
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import DEFAULT_JSON, make_batch  # noqa: E402
+    from mpc_bipedal.config import MPCConfig  # noqa: E402
+    cfg = MPCConfig(**dict(DEFAULT_JSON, horizon=N, strict=False))
+    _, _, zx, zn, x0h, F = make_batch(B, 0, cfg, False)
+    zmax = torch.as_tensor(zx, device="cuda")
+    zmin = torch.as_tensor(zn, device="cuda")
+    x0 = torch.as_tensor(x0h, device="cuda")
+    kick = torch.as_tensor(cfg.dt * F / cfg.m, device="cuda")
+    L = p.rollout_launcher(zmax, zmin, x0, kick=kick, kick_step=n // 2)
+else:
+    zc = np.cumsum(rng.normal(0, 0.01, (B, n, 2)), 1)
+    zmax = torch.as_tensor(zc + 0.05, device="cuda")
+    zmin = torch.as_tensor(zc - 0.05, device="cuda")
+    x0 = torch.zeros((B, 2, 3), dtype=torch.float64, device="cuda")
+    L = p.rollout_launcher(zmax, zmin, x0)
 for _ in range(20):
     L()
 torch.cuda.synchronize()
