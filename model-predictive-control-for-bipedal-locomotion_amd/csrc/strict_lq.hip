@@ -43,6 +43,7 @@
 // (zmpc_strict_lq_table_kernel, the same arithmetic), so a tail slot costs the s recursion twice
 // and the forward step, with no flag loads and no costate.  In sweep A, a segment before the
 // tail in which no lane has a pinned slot runs the free form of the step.
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <cstdlib>
@@ -68,18 +69,22 @@ constexpr bool kLqProf = false;
 #endif
 
 // Riccati steps per checkpoint segment.  Fixed at 8: a segment's working-set flags are one
-// 8-byte LDS word (Flags: [slot / 8][64][8]), which the segment loads, the new-flag writes and
-// the warm-start shift all take whole (rounds 1-3 measured S = 6/10/12/16: slower or spilling).
+// 16-bit LDS word (Flags: [slot / 8][64], 2 bits per slot), which the segment loads, the
+// new-flag writes and the warm-start shift all take whole (rounds 1-3 measured S = 6/10/12/16:
+// slower or spilling).
 constexpr int LQ_S = 8;
 constexpr int LQ_DRIFT = ZMPC_LQ_DRIFT;  // timesteps a lane may run ahead of its wave's slowest lane
                               // (round 3, profiles/r3u/, r3drift/: 0/1/2/4/8 → 104.5/94.8/92.5/
                               // 90.9/92.7 ms at config 3 — the bound rows stay a few rows apart)
+constexpr int kLdsCk = 2;  // at most this many LDS checkpoints per wave (LqArgs::nlck)
 constexpr int TAB = 16;       // doubles per slot of the free-tail table: [0..2] K, [3] 1/Quu,
                               // [4..9] P after the slot (V_k: slots k..N−1 free), [10..12] Qux,
                               // padding
 
 struct LqArgs {
   int N, NS;             // horizon, segments ⌈N/S⌉
+  int nlck;              // working-set checkpoints kept in LDS per wave (0..kLdsCk): those of
+                         // segments jt − 1 .. jt − nlck, sweep A's first and sweep B's last
   int toff;              // window slot k reads time i + toff + k (1 rollout, 0 step)
   int window_mode;
   int64_t n;             // samples per walk (rollout; 1 in window mode)
@@ -123,20 +128,28 @@ struct LqArgs {
   unsigned long long* prof;  // diagnostics build only (ZMPC_LQ_PROF): clocks per phase and axis
 };
 
+// Slot q's flag in a segment's word: its 2-bit field, sign-extended.
+__device__ __forceinline__ int flag_at(unsigned w, int q) {
+  return (int)(w << (30 - 2 * q)) >> 30;
+}
+
+// The 2-bit field of flag value v (−1, 0, +1) at slot q.
+__device__ __forceinline__ unsigned flag_bits(int v, int q) { return (unsigned)(v & 3) << (2 * q); }
+
 template <int S>
 struct SegIn {  // a segment's window slots: z_ref, half-width of the box, working-set flags
-  static_assert(S == 8, "a segment's flags are one 8-byte word of Flags");
+  static_assert(S == 8, "a segment's flags are one 16-bit word of Flags");
   double r[S], h[S];
-  unsigned long long fw;  // the flags, one signed byte per slot: 0 free, +1 at z_max = r + h,
-                          // −1 at z_min = r − h
-  __device__ __forceinline__ int f(int q) const { return (int)(signed char)(fw >> (8 * q)); }
+  unsigned fw;  // the flags, a 2-bit two's-complement field per slot (slot q: bits 2q, 2q + 1):
+                // 0 free, +1 at z_max = r + h, −1 at z_min = r − h
+  __device__ __forceinline__ int f(int q) const { return flag_at(fw, q); }
 };
 
 template <int S>
 struct SegOut {  // a segment's feedback (v = −K η − kff) and forward outputs, per step
   double K0[S], K1[S], K2[S], kf[S];
   double w[S];             // forward: v_k (= T³u_k)
-  unsigned long long fw;   // the segment's new flag word (S = 8): the forward's verdicts on the
+  unsigned fw;             // the segment's new flag word (S = 8): the forward's verdicts on the
                            // free slots, the costate's on the pinned ones; one LDS write
 };
 
@@ -318,25 +331,34 @@ __device__ __forceinline__ void seg_runs(const Lane& L, int t0, RunCursor& c, do
 }
 
 // Per-lane working-set flags of the wave's N slots in LDS (0 free, +1 at z_max, −1 at z_min):
-// one signed byte per slot, [slot / 8][64 lanes][8], so that a lane's segment of 8 slots is one
-// 8-byte word (one conflict-free ds_read_b64 per segment, held packed in the registers).
+// two bits per slot; a lane's 8-slot segment is one 16-bit word (one ds_read_u16 per segment,
+// held packed in a register), two segments one 32-bit bank word of the lane, [slot / 16][64
+// lanes] (so that no two lanes share a bank word).  Every access is a 16-bit one: 32-bit accesses
+// to the same words through another pointer type are not ordered with these by the compiler
+// (type-based aliasing) — a first version that shifted 32 bits at a time computed the same
+// solutions in more passes.
+// Round 6: 2 bits instead of a byte per slot — 128 instead of 512 bytes per segment and wave, so
+// that 8-wave workgroups fit horizons up to 896 (224 with bytes) and the freed LDS holds
+// checkpoints.
 struct Flags {
-  signed char* p;
-  __device__ __forceinline__ static int at(int k, int lane) {
-    return ((k >> 3) * 64 + lane) * 8 + (k & 7);
+  unsigned short* p;
+  __device__ __forceinline__ static int idx(int c, int lane) {
+    return ((c >> 1) * 64 + lane) * 2 + (c & 1);
   }
-  __device__ __forceinline__ int get(int k, int lane) const { return p[at(k, lane)]; }
+  __device__ __forceinline__ int get(int k, int lane) const { return flag_at(word(k >> 3, lane), k & 7); }
   __device__ __forceinline__ void set(int k, int lane, int v) const {
-    p[at(k, lane)] = (signed char)v;
+    const int c = k >> 3, q = k & 7;
+    set_word(c, lane, (word(c, lane) & ~(3u << (2 * q))) | flag_bits(v, q));
   }
   // the 8 flags of slots 8c .. 8c + 7
-  __device__ __forceinline__ unsigned long long word(int c, int lane) const {
-    return *reinterpret_cast<const unsigned long long*>(p + (c * 64 + lane) * 8);
-  }
-  __device__ __forceinline__ void set_word(int c, int lane, unsigned long long w) const {
-    *reinterpret_cast<unsigned long long*>(p + (c * 64 + lane) * 8) = w;
+  __device__ __forceinline__ unsigned word(int c, int lane) const { return p[idx(c, lane)]; }
+  __device__ __forceinline__ void set_word(int c, int lane, unsigned w) const {
+    p[idx(c, lane)] = (unsigned short)w;
   }
 };
+
+// 32-bit flag words of a wave (two segments each)
+__host__ __device__ constexpr int flag_dwords(int NS) { return (NS + 1) / 2; }
 
 // A value function parked in the wave's LDS slot ([9][64] doubles).
 __device__ __forceinline__ void park(double* vp, const Ric& v, int lane) {
@@ -367,7 +389,7 @@ __device__ __forceinline__ void unpark(const double* vp, Ric& v, int lane) {
 
 // A segment's flags as one word (segment j is flag word j).
 template <int S>
-__device__ __forceinline__ unsigned long long seg_flags(const Flags& fl, int j, int lane) {
+__device__ __forceinline__ unsigned seg_flags(const Flags& fl, int j, int lane) {
   return fl.word(j, lane);
 }
 
@@ -470,7 +492,7 @@ __device__ __forceinline__ void seg_forward(const LqArgs& a, int j, const SegIn<
       g.w[q] = u;
       const int nf = (d > ht) ? 1 : ((d < -ht) ? -1 : 0);
       if (in.f(q) == 0) {
-        g.fw |= (unsigned long long)(unsigned char)nf << (8 * q);
+        g.fw |= flag_bits(nf, q);
         changed |= nf != 0;
         kl = nf ? k : kl;  // (slots ascend)
       }
@@ -486,7 +508,7 @@ __device__ __forceinline__ void seg_forward_tail(const LqArgs& a, const double* 
                                                  double* x, double& u0, bool& changed, int& kl,
                                                  const Flags& fl, int lane) {
   const double tol = 1e-13;
-  unsigned long long fw = 0;  // (every slot of a tail segment is free for the lanes taking part)
+  unsigned fw = 0;  // (every slot of a tail segment is free for the lanes taking part)
 #pragma unroll
   for (int q = 0; q < S; ++q) {
     const int k = j * S + q;
@@ -497,7 +519,7 @@ __device__ __forceinline__ void seg_forward_tail(const LqArgs& a, const double* 
       if (k == 0) u0 = u;
       const double d = z - in.r[q], ht = in.h[q] + tol;
       const int nf = (d > ht) ? 1 : ((d < -ht) ? -1 : 0);
-      fw |= (unsigned long long)(unsigned char)nf << (8 * q);
+      fw |= flag_bits(nf, q);
       changed |= nf != 0;
       kl = nf ? k : kl;
     }
@@ -512,7 +534,7 @@ template <int S, bool FULL>
 __device__ __forceinline__ void seg_costate(const LqArgs& a, int j, const SegIn<S>& in,
                                             SegOut<S>& g, double* lam, bool& changed,
                                             int& kl, const Flags& fl, int lane) {
-  unsigned long long& fw = g.fw;  // (written to LDS by the caller)
+  unsigned& fw = g.fw;  // (written to LDS by the caller)
 #pragma unroll
   for (int q = S - 1; q >= 0; --q) {
     const int k = j * S + q;
@@ -524,7 +546,7 @@ __device__ __forceinline__ void seg_costate(const LqArgs& a, int j, const SegIn<
         // wrong-signed multiplier (ν < 0 at z_max, ν > 0 at z_min): σν < −tol
         const bool rel = sg * nu < -a.tolnu;
         if (f != 0) {
-          fw &= rel ? ~(0xffull << (8 * q)) : ~0ull;
+          fw &= rel ? ~(3u << (2 * q)) : ~0u;
           changed |= rel;
           kl = (!rel && k > kl) ? k : kl;
         }
@@ -646,7 +668,7 @@ __device__ __forceinline__ void ck_load_s(const CkIO<NT>& io, const double* ck, 
 // four 64-walk groups, so each SIMD (waves w and w + 4 under the round-robin placement) holds
 // one wave of each axis — the y axis carries nearly all of the active-set work, and an
 // axis-pure SIMD would idle once its x waves are done (config 3: 117 → 98 ms, round 1).  Longer
-// horizons (slot flags of G waves beyond LDS) run G = 4 (x/y = wave parity), 2 or 1.  (Round 4:
+// horizons (slot flags of G waves beyond LDS) run G = 4 (x/y = wave parity) or 2.  (Round 4:
 // waves of 32 walks × both axes, so that every SIMD keeps two y-carrying waves to the end, are
 // slower — config 3 87.0 vs 64.9 ms: the x lanes then run the working-set form up to the wave's
 // last pinned slot, 0.76 of the pass-slots instead of 0.48, profiles/r4/r4l_*.)
@@ -662,15 +684,22 @@ __global__ void __launch_bounds__(64 * G, 2)
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   const int64_t gw = (int64_t)blockIdx.x * G + wave;
   const int N = a.N;
-  // slot flags [NS·S][64] bytes (rows past N stay 0: the last segment's loads are unguarded)
-  const int fbytes = a.NS * S;
-  const Flags fl{reinterpret_cast<signed char*>(lq_smem) + (size_t)wave * fbytes * 64};
+  // slot flags [⌈NS/2⌉][64] 32-bit words (slots past N stay 0: the last segment's loads are
+  // unguarded)
+  const int NSd = flag_dwords(a.NS);
+  const Flags fl{reinterpret_cast<unsigned short*>(lq_smem) + (size_t)wave * NSd * 128};
   // after the G waves' flags: each wave's parked V at the end of its current sweep-B segment
-  // ([9][64] doubles; 16-byte aligned: fbytes·64 is a multiple of 512)
-  double* vpark = reinterpret_cast<double*>(lq_smem + (size_t)G * fbytes * 64) + wave * 12 * 64;
+  // ([9][64] doubles; 16-byte aligned: a wave's flags are ⌈NS/2⌉·256 bytes)
+  double* vpark = reinterpret_cast<double*>(lq_smem + (size_t)G * NSd * 256) +
+                  wave * (12 + 9 * a.nlck) * 64;
   // and behind it the lane's state x (the reference form), [3][64]: read at a pass's start and
   // at its end only, so it need not hold registers through the sweeps
   double* xpark = vpark + 9 * 64;
+  // and behind that the wave's LDS checkpoints ([nlck][9][64] doubles): working-set segments
+  // jt − 1 .. jt − nlck, written first in sweep A and read last in sweep B, so their global
+  // copies were the ones the caches had lost by then (round 6: config 3's checkpoints were
+  // nearly all of its 129 GB per launch)
+  double* ckl = xpark + 3 * 64;
   double* ck = a.ck + (size_t)gw * a.NS * kCkStride;
   const CkIO<NT> io{};
   // work counters, wave-uniform 64-bit sums (scalar registers): wave passes, lane passes (the
@@ -739,7 +768,7 @@ __global__ void __launch_bounds__(64 * G, 2)
     while (L.rt[(rb + 1) * 64 + L.col] <= tB) ++rb;
   }
   const int jfull = N / S;  // segments [0, jfull) are full
-  for (int c = 0; c < fbytes / 8; ++c) fl.set_word(c, lane, 0ull);
+  for (int c = 0; c < 2 * NSd; ++c) fl.set_word(c, lane, 0u);
 
   {
     double x[3] = {0.0, 0.0, 0.0};
@@ -822,8 +851,11 @@ __global__ void __launch_bounds__(64 * G, 2)
             seg_load_runs<S, false, false>(a, j, L, i, rc, fl, cur);
           else
             seg_load<S, false>(a, j, L, i, fl, cur);
-          if (j == 0) park(vpark, v, lane);
-          else ck_store_s(io, ck, j, v, lane);
+          // (s at the end of the last segment is V_N's: 0, no checkpoint)
+          if (j == 0)
+            park(vpark, v, lane);
+          else if (j < a.NS - 1)
+            ck_store_s(io, ck, j, v, lane);
           if (j < jfull)
             seg_tail<S, true, false>(a, tab, j, v, cur, g);
           else
@@ -846,7 +878,10 @@ __global__ void __launch_bounds__(64 * G, 2)
             seg_load_runs<S, true, false>(a, j, L, i, rc, fl, cur);
           else
             seg_load<S, true>(a, j, L, i, fl, cur);
-          ck_store(io, ck, j, v, lane);
+          if (j >= jt - a.nlck)
+            park(ckl + (jt - 1 - j) * 9 * 64, v, lane);
+          else
+            ck_store(io, ck, j, v, lane);
           const bool fr = seg_free(cur);
           if (j < jfull) {
             if (fr)
@@ -887,10 +922,14 @@ __global__ void __launch_bounds__(64 * G, 2)
         if constexpr (RUNS) rc = run_fwd(L, rb);
         // the next segment's checkpoint into v: full for a working-set segment, s for a tail one
         auto next = [&](Ric& w, int j) {
-          if (j + 1 < jt)
+          if (j + 1 < jt - a.nlck)
             ck_load(io, ck, j + 1, w, lane);
-          else if (j + 1 < a.NS)
+          else if (j + 1 < jt)
+            unpark(ckl + (jt - 2 - j) * 9 * 64, w, lane);
+          else if (j + 1 < a.NS - 1)
             ck_load_s(io, ck, j + 1, w, lane);
+          else if (j + 1 == a.NS - 1)
+            w.s0 = w.s1 = w.s2 = 0.0;  // V_N = 0
         };
         // V at the end of segment 0 (later segments' come by `next`); with working-set segments
         // sweep A has left segment 0's feedback in g and V at its end parked: the checkpoint of
@@ -984,15 +1023,17 @@ __global__ void __launch_bounds__(64 * G, 2)
         if (i < a.nsteps) {
           // warm start: the converged set shifted one slot towards the present (slot N−1
           // kept), this lane's column only
-          // (flag words: each word takes its upper 7 bytes and the next word's first)
+          // (flag words: each takes its upper 7 fields and the next word's first; the words past
+          // the one holding the last pinned slot kl are zero and stay zero)
           {
-            const signed char keep = fl.get(N - 1, lane);
-            const int nw = fbytes / 8;
-            unsigned long long w = fl.word(0, lane);
-            for (int c = 0; c < nw; ++c) {
-              const unsigned long long nx = (c + 1 < nw) ? fl.word(c + 1, lane) : 0ull;
-              fl.set_word(c, lane, (w >> 8) | (nx << 56));
-              w = nx;
+            const int keep = fl.get(N - 1, lane);
+            if (kl >= 0) {
+              unsigned w = fl.word(0, lane);
+              for (int c = 0; c <= (kl >> 3); ++c) {
+                const unsigned nx = (c + 1 < a.NS) ? fl.word(c + 1, lane) : 0u;
+                fl.set_word(c, lane, (w >> 2) | ((nx << 14) & 0xffffu));
+                w = nx;
+              }
             }
             fl.set(N - 1, lane, keep);
           }
@@ -1211,23 +1252,31 @@ struct LqVariant {
 #define ZMPC_LQV(G) {G, ZMPC_LQK(G, false), nullptr, nullptr, nullptr, nullptr}
 const LqVariant kLqVariants[] = {
     {8, ZMPC_LQK(8, false), ZMPC_LQK(8, true)},  // default
-    ZMPC_LQV(4),  // N up to 544 (the default G = 8: up to 224)
-    ZMPC_LQV(2),  // N up to 1184
-    ZMPC_LQV(1),  // N up to 2464
+    ZMPC_LQV(4),  // N up to 2176 (the default G = 8: up to 896)
+    ZMPC_LQV(2),  // N up to 2464 (ZMPC_STRICT_MAX_N)
 };
 #undef ZMPC_LQV
 #undef ZMPC_LQK
 constexpr size_t kLdsCap = 160 * 1024;
 
-// LDS of one workgroup: the G waves' slot flags, parked V and state ([12][64] doubles each).
-constexpr size_t lq_lds_bytes(int G, int N) {
-  const size_t rows = (size_t)(N + LQ_S - 1) / LQ_S * LQ_S;
-  return (size_t)G * (rows * 64 + 12 * 64 * sizeof(double));
+// LDS of one workgroup: the G waves' slot flags (2 bits per slot and lane), parked V and state
+// ([12][64] doubles each) and nlck LDS checkpoints ([9][64] doubles each).
+constexpr size_t lq_lds_bytes(int G, int N, int nlck = 0) {
+  const size_t segs = (size_t)(N + LQ_S - 1) / LQ_S;
+  return (size_t)G * ((size_t)flag_dwords((int)segs) * 64 * 4 +
+                      (12 + 9 * (size_t)nlck) * 64 * sizeof(double));
 }
 
-static_assert(lq_lds_bytes(1, ZMPC_STRICT_MAX_N) <= kLdsCap, "ZMPC_STRICT_MAX_N past the LDS");
+// LDS checkpoints per wave that fit beside a workgroup shape (config 3, N = 150: 2 at G = 8)
+int lq_nlck_for(int G, int N) {
+  int c = kLdsCk;
+  while (c > 0 && lq_lds_bytes(G, N, c) > 160 * 1024) --c;
+  return c;
+}
 
-// The largest workgroup whose slot flags and parks fit a CU (N ≤ 2464 at G = 1).
+static_assert(lq_lds_bytes(2, ZMPC_STRICT_MAX_N) <= kLdsCap, "ZMPC_STRICT_MAX_N past the LDS");
+
+// The largest workgroup whose slot flags and parks fit a CU (N ≤ 2464 at G = 2).
 const LqVariant* lq_variant_for(int N) {
   for (const LqVariant& c : kLqVariants)
     if (lq_lds_bytes(c.G, N) <= kLdsCap) return &c;
@@ -1248,7 +1297,11 @@ hipError_t launch_lq(const zmpc_plan* p, LqArgs& a, int64_t waves, hipStream_t s
   const LqVariant* var = lq_variant_for(p->N);
   if (!var) return hipErrorInvalidValue;
   const int64_t blocks = (waves + var->G - 1) / var->G;
-  const size_t lds = lq_lds_bytes(var->G, p->N);
+  a.nlck = lq_nlck_for(var->G, p->N);
+#ifdef ZMPC_DIAG
+  if (const char* e = getenv("ZMPC_LQ_NLCK")) a.nlck = std::min(a.nlck, atoi(e));  // (A/B)
+#endif
+  const size_t lds = lq_lds_bytes(var->G, p->N, a.nlck);
   // cached checkpoints (see CkIO: with run-length bounds the window rows no longer compete
   // for the caches, and non-temporal checkpoints became the slower form — config 3 55.4 vs
   // 56.7 ms, diagnostics build, profiles/r5m/)

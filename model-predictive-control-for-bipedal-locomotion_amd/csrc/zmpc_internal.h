@@ -22,10 +22,9 @@ constexpr int kScanPowOff = 8 * kScanStride;
 constexpr int kScanGOff = kScanPowOff + 8 * 33 * 9;
 constexpr int kScanDoubles = kScanGOff + 8 * 6;
 
-// Longest strict horizon: the LQ kernel's per-wave LDS — slot flags ([N][64] bytes) and the
-// parked V and state (6 KiB, round 5) — must fit a CU for one wave per workgroup
-// (strict_lq.hip lq_variant_for, checked there by a static_assert): N ≤ 2464 (2560 before the
-// parking).
+// Longest strict horizon of the LQ kernel (strict_lq.hip lq_variant_for: its per-wave LDS —
+// slot flags, 2 bits per slot and lane since round 6, and the parked V and state — fits a CU at
+// two waves per workgroup, checked there by a static_assert); unchanged since round 5.
 constexpr int ZMPC_STRICT_MAX_N = 2464;
 
 struct LipmConsts {

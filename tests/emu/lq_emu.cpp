@@ -70,7 +70,9 @@ int main(int argc, char** argv) {
   emu::LqArgs& a = g_args;
   emu::fill_consts(&p, a);
   a.cnt = nullptr;
-  if (emu::lq_lds_bytes(1, N) > sizeof(emu::lq_smem)) return 3;
+  // LDS checkpoints per wave (the kernel's default at N = 150: 2); LQ_EMU_NLCK overrides
+  a.nlck = getenv("LQ_EMU_NLCK") ? atoi(getenv("LQ_EMU_NLCK")) : emu::kLdsCk;
+  if (emu::lq_lds_bytes(1, N, a.nlck) > sizeof(emu::lq_smem)) return 3;
   // the plan's free-tail table (one thread)
   std::vector<double> tab((size_t)N * 16);
   threadIdx.x = 0;

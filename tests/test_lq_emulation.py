@@ -57,13 +57,18 @@ def run_lq(d, exe, zx, zn, N, x0, kick, kstep, form="runs", h=0.75, g=9.81, Q=1.
     return np.frombuffer(r.stdout, np.float64).reshape(n, 2, 3)
 
 
-@pytest.mark.parametrize("N,F,form", ((64, 800, "runs"), (150, 400, "runs"), (64, 0, "rows")))
-def test_lq_kernel_emulated_kicked_walk(emulator, N, F, form):
+@pytest.mark.parametrize("N,F,form,nlck", ((64, 800, "runs", 2), (150, 400, "runs", 2),
+                                            (64, 0, "rows", 2), (150, 800, "runs", 0),
+                                            (150, 800, "runs", 1)))
+def test_lq_kernel_emulated_kicked_walk(emulator, N, F, form, nlck):
+    """nlck: working-set checkpoints kept in LDS per wave (round 6; 2 is the kernel's choice at
+    these horizons, 0 and 1 its choice for longer ones)."""
     d, exe = emulator
     s = golden("strict_ref.npz")
     zx, zn = s[f"n{N}_zmax"], s[f"n{N}_zmin"]
     n = len(zx)
-    h = run_lq(d, exe, zx, zn, N, np.zeros(6), (1.5 / N) * F / 40.0, n // 2, form)
+    h = run_lq(d, exe, zx, zn, N, np.zeros(6), (1.5 / N) * F / 40.0, n // 2, form,
+               env=dict(os.environ, LQ_EMU_NLCK=str(nlck)))
     assert np.abs(h[:, :, 0] - s[f"n{N}_F{F}_com"]).max() <= 1e-12
 
 
