@@ -126,6 +126,7 @@ struct LqArgs {
   int64_t qblock0;       // first block not in the grid
   int64_t nblocks;       // blocks of the whole launch (G waves each)
   unsigned long long* prof;  // diagnostics build only (ZMPC_LQ_PROF): clocks per phase and axis
+  int skip_axis;         // diagnostics build only (ZMPC_LQ_SKIP): 1 / 2 = the x / y tasks end at once
 };
 
 // Slot q's flag in a segment's word: its 2-bit field, sign-extended.
@@ -730,6 +731,9 @@ __global__ void __launch_bounds__(64 * G, 2)
   // bounds follow the positions (table (axis, pos / 64), column pos % 64), everything per walk
   // (x0, kick, history, status) b
   const bool valid = pos < a.B;
+#ifdef ZMPC_DIAG
+  if (a.skip_axis == axis + 1) return;  // (diagnostics: what one axis's tasks cost)
+#endif
   // one resident round (no queue): the y waves carry nearly all the working-set work and set
   // the kernel's time, so they issue first when their SIMD's x wave competes (wave priority;
   // the x waves take the slack) — config 3 50.0 → 45.5 ms.  With the queue the same priority
@@ -1349,6 +1353,7 @@ hipError_t launch_lq(const zmpc_plan* p, LqArgs& a, int64_t waves, hipStream_t s
   }();
   if (prof) (void)hipMemsetAsync(prof, 0, 22 * sizeof(unsigned long long), s);
   a.prof = prof;
+  a.skip_axis = getenv("ZMPC_LQ_SKIP") ? atoi(getenv("ZMPC_LQ_SKIP")) : 0;
 #else
   a.prof = nullptr;
 #endif
