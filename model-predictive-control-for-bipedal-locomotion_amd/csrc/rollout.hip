@@ -711,87 +711,6 @@ __device__ __forceinline__ bool axis_correlate_sparse(const RolloutArgs& a, cons
   return true;
 }
 
-// The same correlation over a per-wave list of the changes (round 6): the ballots' set bits are
-// written once to LDS as (d_m, m) entries (positions from the per-column counts; the area is
-// the history staging's, free until the correlation is done), and one loop walks the list with
-// the next entry's table reads issued before this entry's FMAs.  The bit walk issued each
-// change's reads behind a scalar bit scan, a v_readlane pair and the address arithmetic, with
-// nothing to cover them (four waves per SIMD, all in their own dependent chains).  Same sum,
-// another order of the changes: rounding differs by ≈ε·Σ|S_j d_j|.
-struct ChangeEntry {
-  double d;
-  int m, pad;
-};
-constexpr int kChangeList = 40;  // entries per wave (= kSparseMax)
-
-template <int CW>
-__device__ __forceinline__ bool axis_correlate_sparse_list(const RolloutArgs& a, const double* zr,
-                                                           const double* Ts, ChangeEntry* list,
-                                                           int lane, double* f) {
-  static_assert(kChangeList >= kSparseMax, "the change list holds every sparse wave's changes");
-  using ZL = ZrLayout<CW>;
-  const double* z = zr + ZL::idx(lane * CW);
-  double gv[CW + 1], d[CW];
-  unsigned long long mk[CW];
-  int cnt = 0;
-#pragma unroll
-  for (int j = 0; j <= CW; ++j) gv[j] = z[ZL::idx(j)];
-#pragma unroll
-  for (int q = 0; q < CW; ++q) {
-    d[q] = gv[q + 1] - gv[q];
-    mk[q] = __ballot(d[q] != 0.0);
-    cnt += __popcll(mk[q]);
-  }
-  if (cnt > kSparseMax) return false;
-  const int N = a.hN, s = lane * CW;
-  const unsigned long long lt = (1ull << lane) - 1ull;
-  int base = 0;
-#pragma unroll
-  for (int q = 0; q < CW; ++q) {
-    if ((mk[q] >> lane) & 1ull) {
-      ChangeEntry e;
-      e.d = d[q];
-      e.m = s + q;
-      e.pad = 0;
-      list[base + __popcll(mk[q] & lt)] = e;
-    }
-    base += __popcll(mk[q]);
-  }
-  const double S0 = Ts[ksum_s0(N)];
-#pragma unroll
-  for (int r = 0; r < CW; ++r) f[r] = S0 * gv[r + 1];
-  if (cnt == 0) return true;
-  // f_{s+r} += S_{m−s−r} d_m, S_{e−r} = Ts[e − r + 8] with e = m − s clamped (zeros outside)
-  const double* T0 = Ts + 9 - CW;
-  const int emax = N + CW - 1;
-  auto taps = [&](int c, double* t, double& dv) {
-    const ChangeEntry e = list[c];
-    dv = e.d;
-    const double* p = T0 + min(max(e.m - s, 0), emax);
-#pragma unroll
-    for (int r = 0; r < CW; ++r) t[r] = p[CW - 1 - r];
-  };
-  // entries in pairs, A and B in ping-pong registers; an odd count's last B is entry c again
-  // with d = 0 (adds exact zeros), so that B's reads stay ahead of A's FMAs unconditionally
-  // (the empty asm statements keep each group of reads where it is issued: the compiler would
-  // otherwise sink them to their FMAs)
-  double tA[CW], tB[CW], dA, dB;
-  taps(0, tA, dA);
-  for (int c = 0; c < cnt; c += 2) {
-    const bool two = c + 1 < cnt;  // (uniform)
-    taps(two ? c + 1 : c, tB, dB);
-    asm volatile("" ::: "memory");
-    dB = two ? dB : 0.0;
-#pragma unroll
-    for (int r = 0; r < CW; ++r) f[r] = fma(tA[r], dA, f[r]);
-    taps(c + 2 < cnt ? c + 2 : c, tA, dA);
-    asm volatile("" ::: "memory");
-#pragma unroll
-    for (int r = 0; r < CW; ++r) f[r] = fma(tB[r], dB, f[r]);
-  }
-  return true;
-}
-
 // Split-axis kernel, one walk per 128-thread workgroup: wave 0 solves the x axis and wave 1 the
 // y axis (half the registers and twice the waves of the one-wave kernel, for latency hiding);
 // they share the staged z_ref and the history staging rows, so loads and stores stay whole-walk
@@ -869,11 +788,8 @@ __device__ __forceinline__ void split_walk(const RolloutArgs& a, int64_t b, doub
     tl_stamp(a, b, 1);
     // ---- 3. correlation (this wave's axis) -------------------------------------------------
     // sparse z_ref differences (piecewise-constant CoP) first, else the dense forms
-    // (the change lists behind the table, in the staging area that the correlation leaves free)
-    ChangeEntry* list = reinterpret_cast<ChangeEntry*>(Ts + ((ksum_rows(a.hN) + 1) & ~1)) +
-                        axis * kChangeList;
     const bool sparse = a.ksum != nullptr && !dbgb(a, 1) &&
-                        axis_correlate_sparse_list<CW>(a, axis ? zr1 : zr0, Ts, list, lane, f);
+                        axis_correlate_sparse<CW>(a, axis ? zr1 : zr0, Ts, lane, f);
     if (sparse) {
     } else if constexpr (FFA && (CW & 1))
       axis_correlate_ffa<CW>(a, kg, axis ? zr1 : zr0, lane, f);  // kg = the fast-FIR taps
@@ -1856,8 +1772,7 @@ void launch_unc(const RolloutGeom& g, size_t lds, hipStream_t s, RolloutArgs a, 
   const size_t lds_axis = lds - (size_t)a.kcp * sizeof(double);  // no staged gain row
   size_t lds_split = std::max<size_t>(lds_axis, HistLayout<CW>::doubles(a.n) * sizeof(double));
   // the sparse-difference correlation stages the plan's suffix sums behind the z_ref areas
-  const size_t lds_sparse = std::max(lds_axis + (size_t)((ksum_rows(a.hN) + 1) & ~1) * sizeof(double) +
-                                         2 * kChangeList * sizeof(ChangeEntry),
+  const size_t lds_sparse = std::max(lds_axis + (size_t)ksum_rows(a.hN) * sizeof(double),
                                      lds_split);
   if (a.ksum != nullptr && lds_sparse <= 64 * 1024)
     lds_split = lds_sparse;
