@@ -32,7 +32,9 @@
 // slot is V there.  The working-set iteration, its warm start (the previous timestep's set
 // shifted one slot, slot N−2 freed, N−1 kept) and the state advance in the reference form are
 // the LQ kernel's, so both kernels converge to the same sets and agree to rounding.
+#include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 
 #include "strict_eta.h"
 #include "zmpc_internal.h"
@@ -632,9 +634,13 @@ int lanes_per_instance(const zmpc_plan* p, int64_t ninst) {
 
 hipError_t launch(const zmpc_plan* p, const ScanArgs& a, hipStream_t s, int L) {
   const dim3 blk(64);
+  int cmin = 1;
+#ifdef ZMPC_DIAG
+  if (const char* e = getenv("ZMPC_SCAN_CMIN")) cmin = atoi(e);  // (diagnostics: wider chunks)
+#endif
   if (L == 32) {
     const dim3 grid((unsigned)((a.ninst + 1) / 2));
-    switch ((p->N + 31) / 32) {
+    switch (std::max((p->N + 31) / 32, std::min(cmin, 16))) {
 #define ZMPC_SCASE(CC)                                                        \
   case CC:                                                                    \
     hipLaunchKernelGGL((zmpc_strict_scan_kernel<CC, 32>), grid, blk, 0, s, a); \

@@ -21,6 +21,8 @@
 #                                      step name (pyd:...) loads the diagnostics build
 #   sq:<B>                             SQ instruction / wait counters of the unconstrained rollout
 #                                      (scripts/gpu_rollout_pmc.sh, CoP walks)
+#   envsweep:<VAR>:<value>:<LO:HI:STEP> the diagnostics build's horizon sweep (strict leg) with an
+#                                      environment switch set
 #   res                                register/scratch report of every kernel (host-side, no GPU)
 set -u
 TAG=$1
@@ -102,6 +104,13 @@ PY
     sq)
       bash scripts/gpu_rollout_pmc.sh "$TAG/sq" "$rest" > "$OUT/sq.log" 2>&1
       rc=$?; tail -3 "$OUT/sq.log"; step sq $rc ;;
+    envsweep)
+      var=${rest%%:*}; rest=${rest#*:}; v=${rest%%:*}; rng=${rest#*:}
+      env ZMPC_LIB=$PWD/model-predictive-control-for-bipedal-locomotion_amd/mpc_bipedal/libzmpc_diag.so \
+        $var=$v timeout -k 10 600 python bench.py --sweep-horizon $rng --no-cpu-baseline \
+        > "$OUT/envsweep_${var}_$v.jsonl" 2> "$OUT/envsweep_${var}_$v.err"
+      rc=$?; python -c "import json,sys; [print(d['N'], '%.3e' % d['gpu_batched_strict']) for d in map(json.loads, open(sys.argv[1])) if 'N' in d]" "$OUT/envsweep_${var}_$v.jsonl"
+      step envsweep $rc ;;
     res)
       for f in rollout strict_lq strict_scan herdt; do
         make -s -C model-predictive-control-for-bipedal-locomotion_amd/csrc resources RES=$f
