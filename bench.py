@@ -1079,7 +1079,8 @@ def rollout_bench(args, conf, rank, world, dev, dist_on):
                     "passes_per_solve": work["instance_passes"] / per / (B * (n - 1) * 2),
                     "max_passes_per_solve": work["max_passes_per_solve"],
                     "lane_efficiency": work["instance_passes"] / max(1, 64 * work["wave_passes"]),
-                    "working_set_slot_frac": ws / max(1, slots)}
+                    "working_set_slot_frac": ws / max(1, slots),
+                    "traffic_over_alg_bytes": (traffic / alg_bytes if traffic else None)}
         roof.update({
             "traffic": traffic,
             "kernel": rollout_kernel_name(B, n, cfg.horizon, cfg.strict, wl["shared"]),

@@ -1201,6 +1201,9 @@ __global__ void __launch_bounds__(128 * W, E == 4 ? 6 : 4) zmpc_rollout_unc_wide
   double* zr0 = smem;
   double* zr1 = zr0 + a.lzp;
   __shared__ int scnt[2][W];  // per-wave z_ref change counts (sparse attempt)
+  // (diagnostics timeline: [0] start, [1] correlation inputs staged, [2] correlation done,
+  // [3] scan and cross-wave chain done, [4] last copy-out issued)
+  tl_stamp(a, b, 0);
   double* Ts = smem + 2 * a.lzp;  // sparse attempt: suffix sums, then the change lists
   double* ld = Ts + ((ksum_rows(a.hN) + 1) & ~1);
   int* lm = reinterpret_cast<int*>(ld + 2 * kSparseMaxWide);
@@ -1232,6 +1235,7 @@ __global__ void __launch_bounds__(128 * W, E == 4 ? 6 : 4) zmpc_rollout_unc_wide
         zr1[ZL::idx(t)] = (hi.y + lo.y) / 2;
       }
       __syncthreads();
+      tl_stamp(a, b, 1);
       dense = !wide_correlate_sparse<CW, W>(a, axis ? zr1 : zr0, Ts, ld, lm, scnt, axis, w, lane,
                                              f);
     }
@@ -1290,6 +1294,7 @@ __global__ void __launch_bounds__(128 * W, E == 4 ? 6 : 4) zmpc_rollout_unc_wide
         !wide_correlate_sparse<CW, W>(a, axis ? zr1 : zr0, Ts, ld, lm, scnt, axis, w, lane, f))
       axis_correlate<CW>(a, a.k, (axis ? zr1 : zr0) + ZL::idx(w * 64 * CW), lane, f);
   }
+  tl_stamp(a, b, 2);
   const double* xb = a.x0 + b * 6 + 3 * axis;
   const double xi[3] = {xb[0], xb[1], xb[2]};
   const double kk = (axis == 1 && a.kick != nullptr) ? a.kick[b] : 0.0;
@@ -1382,6 +1387,7 @@ __global__ void __launch_bounds__(128 * W, E == 4 ? 6 : 4) zmpc_rollout_unc_wide
     const double p = __shfl_up(sv[i], 1, 64);
     xs0[i] = (lane == 0) ? xs[i] : p;
   }
+  tl_stamp(a, b, 3);
   // ---- 4. replay (reference form) into the staging rows, coalesced copy-out per round --------
   // staging rows padded as the split kernels' (HistLayout: two doubles after every CW local
   // rows, even CW), so the lanes' ds_write rows are not 128 B multiples apart
@@ -1441,6 +1447,7 @@ __global__ void __launch_bounds__(128 * W, E == 4 ? 6 : 4) zmpc_rollout_unc_wide
       a.status[b] = fl;
     }
   }
+  tl_stamp(a, b, 4);
   if (a.dbg < 0) a.hist[tid] = pf0 + pf1;  // never (dbg ≥ 0): keeps the prefetch loads
 }
 

@@ -64,6 +64,7 @@ struct ScanArgs {
   // z-form step constants (strict_eta.h fill_eta)
   double pi, ipi, ipi2, gp, rho, eps, epsg, epsg2, quz0, epi, tolnu;
   double iR, piR, rhoR, rhoP2;  // slot elements: 1/R, π/R, ρ/R, ρ/π² (R = π² + ρ)
+  int dbg_noshfl;  // diagnostics build only (ZMPC_SCAN_NOSHFL): no element shuffles (timing)
 };
 
 // symmetric 3×3 in 6 doubles: 00 01 02 11 12 22
@@ -392,7 +393,12 @@ __global__ void __launch_bounds__(64, (C >= ZMPC_SCAN_ONE_WAVE_C ? 1 : 2))
 #pragma unroll
         for (int d = 1; d < L; d <<= 1) {
           Elem P;
-          shfl_down_elem(E, P, d);
+#ifdef ZMPC_DIAG
+          if (a.dbg_noshfl)  // (diagnostics: the element scan's cost without its shuffles)
+            P = E;
+          else
+#endif
+            shfl_down_elem(E, P, d);
           if (il + d < L) combine(E, P);
         }
         // V at the chunk's end = the right neighbour's suffix (0 past the horizon).  Every lane
@@ -617,6 +623,9 @@ void fill(const zmpc_plan* p, ScanArgs& a) {
   a.N = p->N;
   fill_consts(a, p->T, p->T2_2, p->T3_6, p->hg, p->Q, p->R);
   a.cnt = p->lqcnt;
+#ifdef ZMPC_DIAG
+  a.dbg_noshfl = getenv("ZMPC_SCAN_NOSHFL") != nullptr;
+#endif
 }
 
 // Lanes per instance: a whole wave while the instances fit one wave per SIMD (the latency of

@@ -1,4 +1,5 @@
-"""Diagnostic: per-walk phase timeline of the unconstrained split kernel (diagnostics build,
+"""Diagnostic: per-walk phase timeline of the unconstrained split kernel, or of the wide kernel
+for walks of more than 513 samples (diagnostics build,
 ZMPC_ROLLOUT_TL): each walk's wave 0 stamps the 100 MHz constant clock at its start, once its
 bounds are in LDS, after the correlation, after the staged history and after issuing the copy-out.
 Prints the mean phase durations per dispatch round and a chip-wide occupancy profile (walks in
@@ -42,8 +43,10 @@ start = t[:, 0]
 # dispatch rounds: a walk that starts after the first walk to end is a later round
 first_end = t[:, 4].min()
 rnd = (start > first_end).astype(int)
+split = n - 1 <= 512
 out = {"B": B, "N": N, "n": n, "span_us": float(t[:, 4].max()),
-       "phases": ["load+stage", "correlation", "scan+replay", "copy-out issue"]}
+       "phases": ["load+stage", "correlation", "scan+replay", "copy-out issue"] if split else
+       ["load+stage", "correlation", "scan+chain", "replay+copy-out rounds"]}
 for r in (0, 1):
     m = rnd == r
     if m.any():
