@@ -64,7 +64,6 @@ struct ScanArgs {
   // z-form step constants (strict_eta.h fill_eta)
   double pi, ipi, ipi2, gp, rho, eps, epsg, epsg2, quz0, epi, tolnu;
   double iR, piR, rhoR, rhoP2;  // slot elements: 1/R, π/R, ρ/R, ρ/π² (R = π² + ρ)
-  int dbg_noshfl;  // diagnostics build only (ZMPC_SCAN_NOSHFL): no element shuffles (timing)
 };
 
 // symmetric 3×3 in 6 doubles: 00 01 02 11 12 22
@@ -270,17 +269,77 @@ __device__ __forceinline__ void combine(Elem& e1, const Elem& e2) {
   for (int q = 0; q < 3; ++q) e1.b[q] = bn[q];
 }
 
-__device__ __forceinline__ void shfl_down_elem(const Elem& e, Elem& o, int d) {
+__device__ __forceinline__ void shfl_elem(const Elem& e, Elem& o, int src) {
 #pragma unroll
-  for (int q = 0; q < 9; ++q) o.A[q] = __shfl_down(e.A[q], d, 64);
+  for (int q = 0; q < 9; ++q) o.A[q] = __shfl(e.A[q], src, 64);
 #pragma unroll
-  for (int q = 0; q < 3; ++q) o.b[q] = __shfl_down(e.b[q], d, 64);
+  for (int q = 0; q < 3; ++q) o.b[q] = __shfl(e.b[q], src, 64);
 #pragma unroll
-  for (int q = 0; q < 6; ++q) o.C[q] = __shfl_down(e.C[q], d, 64);
+  for (int q = 0; q < 6; ++q) o.C[q] = __shfl(e.C[q], src, 64);
 #pragma unroll
-  for (int q = 0; q < 3; ++q) o.g[q] = __shfl_down(e.g[q], d, 64);
+  for (int q = 0; q < 3; ++q) o.g[q] = __shfl(e.g[q], src, 64);
 #pragma unroll
-  for (int q = 0; q < 6; ++q) o.J[q] = __shfl_down(e.J[q], d, 64);
+  for (int q = 0; q < 6; ++q) o.J[q] = __shfl(e.J[q], src, 64);
+}
+
+// A DPP lane move of a double (two 32-bit moves on the VALU, no LDS pipe) into the rows of
+// ROWS (the others read 0); lanes whose source is invalid read 0 (bound_ctrl).
+template <int CTRL, int ROWS = 0xF>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, ROWS, 0xF, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, ROWS, 0xF, true);
+  return __hiloint2double(hi, lo);
+}
+// wave_shl:1 / wave_shr:1 — lane i reads lane i + 1 / i − 1 across the whole wave (the instance
+// boundaries are the callers' business)
+__device__ __forceinline__ double next_lane_f64(double v) { return dpp_f64<0x130>(v); }
+__device__ __forceinline__ double prev_lane_f64(double v) { return dpp_f64<0x138>(v); }
+
+// the lane d behind inside the row (row_shr:d, d = 1, 2, 4, 8), or, for d = 16 / 32, the last
+// lane of the previous 16 / 32-lane block (row_bcast:15 into rows 1, 3; row_bcast:31 into rows
+// 2, 3) — the Kogge-Stone prefix levels of an aligned L-lane instance
+__device__ __forceinline__ double prefix_src_f64(double v, int d) {
+  switch (d) {
+    case 1:
+      return dpp_f64<0x111>(v);
+    case 2:
+      return dpp_f64<0x112>(v);
+    case 4:
+      return dpp_f64<0x114>(v);
+    case 8:
+      return dpp_f64<0x118>(v);
+    case 16:
+      return dpp_f64<0x142, 0xA>(v);
+    default:
+      return dpp_f64<0x143, 0xC>(v);
+  }
+}
+
+// row_shl:d — lane i reads lane i + d of its row (d = 1, 2, 4, 8)
+__device__ __forceinline__ double row_shl_f64(double v, int d) {
+  switch (d) {
+    case 1:
+      return dpp_f64<0x101>(v);
+    case 2:
+      return dpp_f64<0x102>(v);
+    case 4:
+      return dpp_f64<0x104>(v);
+    default:
+      return dpp_f64<0x108>(v);
+  }
+}
+
+__device__ __forceinline__ void row_shl_elem(const Elem& e, Elem& o, int d) {
+#pragma unroll
+  for (int q = 0; q < 9; ++q) o.A[q] = row_shl_f64(e.A[q], d);
+#pragma unroll
+  for (int q = 0; q < 3; ++q) o.b[q] = row_shl_f64(e.b[q], d);
+#pragma unroll
+  for (int q = 0; q < 6; ++q) o.C[q] = row_shl_f64(e.C[q], d);
+#pragma unroll
+  for (int q = 0; q < 3; ++q) o.g[q] = row_shl_f64(e.g[q], d);
+#pragma unroll
+  for (int q = 0; q < 6; ++q) o.J[q] = row_shl_f64(e.J[q], d);
 }
 
 // One wave per workgroup holding 64/L instances of L lanes each; lane l of an instance owns
@@ -390,16 +449,20 @@ __global__ void __launch_bounds__(64, (C >= ZMPC_SCAN_ONE_WAVE_C ? 1 : 2))
             prepend(a, al, b2s, c22, ka, gc, E);
           }
         }
+        // suffix scan: inside each 16-lane row on DPP moves (the lane d ahead, d = 1, 2, 4, 8),
+        // then across rows, each lane of an aligned block's first half taking the suffix of the
+        // second half's first lane (one LDS-pipe shuffle level per doubling of 16)
 #pragma unroll
-        for (int d = 1; d < L; d <<= 1) {
+        for (int d = 1; d < 16; d <<= 1) {
           Elem P;
-#ifdef ZMPC_DIAG
-          if (a.dbg_noshfl)  // (diagnostics: the element scan's cost without its shuffles)
-            P = E;
-          else
-#endif
-            shfl_down_elem(E, P, d);
-          if (il + d < L) combine(E, P);
+          row_shl_elem(E, P, d);
+          if ((il & 15) + d < 16) combine(E, P);
+        }
+#pragma unroll
+        for (int d = 16; d < L; d <<= 1) {
+          Elem P;
+          shfl_elem(E, P, base + (il & ~(2 * d - 1)) + d);
+          if ((il & d) == 0) combine(E, P);
         }
         // V at the chunk's end = the right neighbour's suffix (0 past the horizon).  Every lane
         // takes part in the shuffles (a source lane outside the exec mask reads as 0); the last
@@ -407,9 +470,9 @@ __global__ void __launch_bounds__(64, (C >= ZMPC_SCAN_ONE_WAVE_C ? 1 : 2))
         {
           double vv[9];
 #pragma unroll
-          for (int q = 0; q < 6; ++q) vv[q] = __shfl_down(E.J[q], 1, 64);
+          for (int q = 0; q < 6; ++q) vv[q] = next_lane_f64(E.J[q]);
 #pragma unroll
-          for (int q = 0; q < 3; ++q) vv[6 + q] = __shfl_down(E.g[q], 1, 64);
+          for (int q = 0; q < 3; ++q) vv[6 + q] = next_lane_f64(E.g[q]);
           const bool last = il == L - 1;
           v.p00 = last ? 0.0 : vv[0];
           v.p01 = last ? 0.0 : vv[1];
@@ -461,10 +524,11 @@ __global__ void __launch_bounds__(64, (C >= ZMPC_SCAN_ONE_WAVE_C ? 1 : 2))
       for (int d = 1; d < L; d <<= 1) {
         double Fp[9], pp[3];
 #pragma unroll
-        for (int q = 0; q < 9; ++q) Fp[q] = __shfl_up(F[q], d, 64);
+        for (int q = 0; q < 9; ++q) Fp[q] = prefix_src_f64(F[q], d);
 #pragma unroll
-        for (int q = 0; q < 3; ++q) pp[q] = __shfl_up(ph[q], d, 64);
-        if (il >= d) {  // (F, φ) ← (F, φ) ∘ (Fp, pp): the earlier lanes' map first
+        for (int q = 0; q < 3; ++q) pp[q] = prefix_src_f64(ph[q], d);
+        if (d < 16 ? (il & 15) >= d : (il & d) != 0) {  // (F, φ) ← (F, φ) ∘ (Fp, pp): the
+                                                        // earlier lanes' map first
           double Fn[9], pn[3];
 #pragma unroll
           for (int i2 = 0; i2 < 3; ++i2) {
@@ -487,7 +551,7 @@ __global__ void __launch_bounds__(64, (C >= ZMPC_SCAN_ONE_WAVE_C ? 1 : 2))
           xe[i2] = fma(F[3 * i2], e0[0], fma(F[3 * i2 + 1], e0[1], fma(F[3 * i2 + 2], e0[2], ph[i2])));
 #pragma unroll
         for (int i2 = 0; i2 < 3; ++i2) {
-          const double up = __shfl_up(xe[i2], 1, 64);
+          const double up = prev_lane_f64(xe[i2]);
           xs[i2] = il == 0 ? e0[i2] : up;
         }
       }
@@ -502,7 +566,7 @@ __global__ void __launch_bounds__(64, (C >= ZMPC_SCAN_ONE_WAVE_C ? 1 : 2))
         ls[2] = fma(v.p02, xs[0], fma(v.p12, xs[1], v.p22 * xs[2])) - v.s2;
 #pragma unroll
         for (int i2 = 0; i2 < 3; ++i2) {
-          const double dn = __shfl_down(ls[i2], 1, 64);
+          const double dn = next_lane_f64(ls[i2]);
           lam[i2] = il == L - 1 ? 0.0 : dn;
         }
       }
@@ -577,7 +641,7 @@ __global__ void __launch_bounds__(64, (C >= ZMPC_SCAN_ONE_WAVE_C ? 1 : 2))
     }
     // warm start: the set shifted one slot towards the present, slot N−2 freed, N−1 kept
     {
-      const int nxt = __shfl_down(f[0], 1, 64);
+      const int nxt = __builtin_amdgcn_update_dpp(0, f[0], 0x130, 0xF, 0xF, true);  // wave_shl:1
       int g[C];
 #pragma unroll
       for (int q = 0; q < C; ++q) {
@@ -624,7 +688,6 @@ void fill(const zmpc_plan* p, ScanArgs& a) {
   fill_consts(a, p->T, p->T2_2, p->T3_6, p->hg, p->Q, p->R);
   a.cnt = p->lqcnt;
 #ifdef ZMPC_DIAG
-  a.dbg_noshfl = getenv("ZMPC_SCAN_NOSHFL") != nullptr;
 #endif
 }
 

@@ -23,6 +23,7 @@
 #                                      (scripts/gpu_rollout_pmc.sh, CoP walks)
 #   envsweep:<VAR>:<value>:<LO:HI:STEP> the diagnostics build's horizon sweep (strict leg) with an
 #                                      environment switch set
+#   sweep:<name>:<lib|->:<LO:HI:STEP>  the horizon sweep with the product library or another one
 #   res                                register/scratch report of every kernel (host-side, no GPU)
 set -u
 TAG=$1
@@ -111,6 +112,14 @@ PY
         > "$OUT/envsweep_${var}_$v.jsonl" 2> "$OUT/envsweep_${var}_$v.err"
       rc=$?; python -c "import json,sys; [print(d['N'], '%.3e' % d['gpu_batched_strict']) for d in map(json.loads, open(sys.argv[1])) if 'N' in d]" "$OUT/envsweep_${var}_$v.jsonl"
       step envsweep $rc ;;
+    sweep)
+      name=${rest%%:*}; rest=${rest#*:}; lib=${rest%%:*}; rng=${rest#*:}
+      L=()
+      [ "$lib" != "-" ] && L=(env ZMPC_LIB=$PWD/$lib)
+      timeout -k 10 600 "${L[@]}" python bench.py --sweep-horizon $rng --no-cpu-baseline \
+        > "$OUT/sweep_$name.jsonl" 2> "$OUT/sweep_$name.err"
+      rc=$?; python -c "import json,sys; [print(sys.argv[2], d['N'], '%.3e' % d['gpu_batched_strict']) for d in map(json.loads, open(sys.argv[1])) if 'N' in d]" "$OUT/sweep_$name.jsonl" "$name"
+      step "sweep $name" $rc ;;
     res)
       for f in rollout strict_lq strict_scan herdt; do
         make -s -C model-predictive-control-for-bipedal-locomotion_amd/csrc resources RES=$f

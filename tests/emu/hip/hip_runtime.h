@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <cstdlib>
 using std::fabs;
 using std::fma;
 using std::isfinite;
@@ -62,6 +63,52 @@ inline T __shfl_xor(T v, int m, int = 64) {
 template <class T>
 inline T __shfl(T v, int s, int = 64) {
   return emu_xchg(v, s);
+}
+inline int __double2loint(double v) {
+  uint64_t u;
+  std::memcpy(&u, &v, 8);
+  return (int)(uint32_t)u;
+}
+inline int __double2hiint(double v) {
+  uint64_t u;
+  std::memcpy(&u, &v, 8);
+  return (int)(uint32_t)(u >> 32);
+}
+inline double __hiloint2double(int hi, int lo) {
+  const uint64_t u = ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+  double v;
+  std::memcpy(&v, &u, 8);
+  return v;
+}
+// DPP lane moves: row_shl:n (0x101-0x10F) and row_shr:n (0x111-0x11F) inside 16-lane rows,
+// wave_shl:1 (0x130), wave_shr:1 (0x138), row_bcast:15 (0x142: row r reads lane 16r − 1) and
+// row_bcast:31 (0x143: rows 2, 3 read lane 31).  Rows outside row_mask keep `old`; an invalid
+// source reads 0 under bound_ctrl, else `old`.
+inline int __builtin_amdgcn_update_dpp(int old, int src, int ctrl, int row_mask, int bank_mask,
+                                       bool bound_ctrl) {
+  const int l = (int)threadIdx.x;
+  int from = -1;
+  if (ctrl > 0x100 && ctrl < 0x110) {
+    const int n = ctrl - 0x100;
+    if ((l & 15) + n < 16) from = l + n;
+  } else if (ctrl > 0x110 && ctrl < 0x120) {
+    const int n = ctrl - 0x110;
+    if ((l & 15) >= n) from = l - n;
+  } else if (ctrl == 0x130) {
+    if (l < 63) from = l + 1;
+  } else if (ctrl == 0x138) {
+    if (l > 0) from = l - 1;
+  } else if (ctrl == 0x142) {
+    if (l >= 16) from = (l & ~15) - 1;
+  } else if (ctrl == 0x143) {
+    if (l >= 32) from = 31;
+  } else {
+    std::abort();  // (a DPP control the emulation does not model)
+  }
+  if (bank_mask != 0xF) std::abort();
+  const int v = emu_xchg(src, from >= 0 ? from : l);
+  if (!((row_mask >> (l >> 4)) & 1)) return old;
+  return from >= 0 ? v : (bound_ctrl ? 0 : old);
 }
 inline bool __any(bool b) {
   emu_buf[threadIdx.x] = b;
