@@ -1820,6 +1820,21 @@ void launch_unc(const RolloutGeom& g, size_t lds, hipStream_t s, RolloutArgs a, 
 
 size_t zmpc_rollout_unc_lds_bytes(int N, int64_t n) { return lds_bytes(rollout_geom(N, n)); }
 
+#ifdef ZMPC_DIAG
+// diagnostics: the phase stamps of the last launch to $ZMPC_ROLLOUT_TL ([B][5] u64)
+static void tl_write(const unsigned long long* tl, int64_t B, hipStream_t s, hipError_t e) {
+  const char* path = getenv("ZMPC_ROLLOUT_TL");
+  if (tl == nullptr || path == nullptr || e != hipSuccess) return;
+  std::vector<unsigned long long> h((size_t)B * 5);
+  (void)hipStreamSynchronize(s);
+  (void)hipMemcpy(h.data(), tl, h.size() * 8, hipMemcpyDeviceToHost);
+  if (FILE* f = fopen(path, "wb")) {
+    fwrite(h.data(), 8, h.size(), f);
+    fclose(f);
+  }
+}
+#endif
+
 hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, const double* zmax,
                                    const double* zmin, int64_t bstride, const double* x0,
                                    const double* kick, int64_t kick_step,
@@ -1871,12 +1886,11 @@ hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, con
   a.ksum = p->opt[ZMPC_OPT_CORRELATION] == 1 ? nullptr : p->ksum;
   a.hN = p->N;
 #ifdef ZMPC_DIAG
-  // diagnostics: per-walk phase stamps of the split kernel, written to $ZMPC_ROLLOUT_TL after
+  // diagnostics: per-walk phase stamps of the split and wide kernels, written to $ZMPC_ROLLOUT_TL after
   // every launch ([B][5] u64, wall_clock64 ticks)
-  static const char* tl_path = getenv("ZMPC_ROLLOUT_TL");
   static unsigned long long* tl_buf = nullptr;
   static int64_t tl_cap = 0;
-  if (tl_path && B > tl_cap) {
+  if (getenv("ZMPC_ROLLOUT_TL") && B > tl_cap) {
     if (tl_buf) (void)hipFree(tl_buf);
     tl_buf = nullptr;
     tl_cap = hipMalloc((void**)&tl_buf, (size_t)B * 5 * 8) == hipSuccess ? B : 0;
@@ -1941,7 +1955,11 @@ hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, con
       default:
         return hipErrorInvalidValue;
     }
-    return hipGetLastError();
+    const hipError_t ew = hipGetLastError();
+#ifdef ZMPC_DIAG
+    tl_write(a.tl, B, s, ew);
+#endif
+    return ew;
   }
   // shared CoP (bounds stride 0) with a single-pass geometry: f once per launch
   double* fsh = nullptr;
@@ -1969,15 +1987,7 @@ hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, con
   }
   hipError_t e = hipGetLastError();
 #ifdef ZMPC_DIAG
-  if (a.tl && e == hipSuccess) {
-    std::vector<unsigned long long> h((size_t)B * 5);
-    (void)hipStreamSynchronize(s);
-    (void)hipMemcpy(h.data(), a.tl, h.size() * 8, hipMemcpyDeviceToHost);
-    if (FILE* f = fopen(tl_path, "wb")) {
-      fwrite(h.data(), 8, h.size(), f);
-      fclose(f);
-    }
-  }
+  tl_write(a.tl, B, s, e);
 #endif
   if (fsh) {
     const hipError_t ef = hipFreeAsync(fsh, s);
