@@ -140,7 +140,7 @@ int zmpc_plan_timings(const zmpc_plan* plan, float* dst_host, int32_t count);
  *                           Cholesky tile kernel (16 instances per workgroup; cross-check),
  *                           2 = the reduced-Cholesky one-instance-per-wavefront kernel
  *                           (cross-check), 3 = the LQ kernel, 4 = the parallel-in-time kernel
- *                           (1, 2 and 4: horizons up to 512)
+ *                           (1 and 2: horizons up to 512; 4: up to 960)
  *   ZMPC_OPT_STRICT_BOUNDS  strict rollouts on the LQ kernel: 0 = auto (run-length bounds;
  *                           rows for a shared CoP before round 5), 1 = the bounds staged one row
  *                           per sample, 2 = run-length bounds (one entry per run of equal

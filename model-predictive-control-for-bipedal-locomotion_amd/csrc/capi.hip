@@ -248,10 +248,12 @@ int zmpc_plan_set_option(zmpc_plan* P, int32_t option, int64_t value) {
   if (option < 0 || option >= ZMPC_NOPTIONS) return fail(ZMPC_EINVAL, "unknown option");
   if (value < 0 || value > hi[option])
     return fail(ZMPC_EINVAL, "option value out of range (0.." + std::to_string(hi[option]) + ")");
-  if (option == ZMPC_OPT_STRICT_SOLVER && (value == 1 || value == 2 || value == 4) &&
+  if (option == ZMPC_OPT_STRICT_SOLVER && (value == 1 || value == 2) &&
       (!P->strict || P->N > 512))
-    return fail(ZMPC_EINVAL, "the small-batch and reduced-Cholesky strict kernels need a strict "
-                             "plan, N <= 512");
+    return fail(ZMPC_EINVAL, "the reduced-Cholesky strict kernels need a strict plan, N <= 512");
+  if (option == ZMPC_OPT_STRICT_SOLVER && value == 4 &&
+      (!P->strict || !zmpc_strict_scan_supported(P)))
+    return fail(ZMPC_EINVAL, "the small-batch strict kernel needs a strict plan, N <= 960");
   if (option == ZMPC_OPT_STRICT_SOLVER && value == 3 && !zmpc_strict_lq_supported(P))
     return fail(ZMPC_EINVAL, "the LQ strict kernel needs a strict plan, N <= " +
                                   std::to_string(ZMPC_STRICT_MAX_N));

@@ -44,6 +44,10 @@ namespace {
 using namespace zmpc_eta;
 
 constexpr int SC_MAXIT = 64;  // active-set pass cap (as strict_lq.hip)
+// horizons of the kernel: 32-lane instances to N = 512 (C ≤ 16 slots per lane: 256 VGPRs + 248
+// AGPRs), whole-wave ones to 960 (C ≤ 15: 256 + 236; C = 16 of 64 lanes spills 12 B to scratch)
+constexpr int kScan32MaxN = 512;
+constexpr int kScanMaxN = 960;
 
 struct ScanArgs {
   int N;
@@ -687,13 +691,11 @@ void fill(const zmpc_plan* p, ScanArgs& a) {
   a.N = p->N;
   fill_consts(a, p->T, p->T2_2, p->T3_6, p->hg, p->Q, p->R);
   a.cnt = p->lqcnt;
-#ifdef ZMPC_DIAG
-#endif
 }
 
 // Lanes per instance: a whole wave while the instances fit one wave per SIMD (the latency of
 // one pass is what counts), 32 beyond (two instances per wave; chunks of up to 16 slots,
-// N ≤ 512: N = 330–510 at 1024 walks 8.3e7–9.1e7 → 1.26e8–1.40e8 solves/s, profiles/r5aa/).  Chunks of C ≥ 3 slots per lane hold 1 wave per SIMD (their state spills past 256
+// N ≤ 512; whole-wave instances beyond, to N = 960: N = 330–510 at 1024 walks 8.3e7–9.1e7 → 1.26e8–1.40e8 solves/s, profiles/r5aa/).  Chunks of C ≥ 3 slots per lane hold 1 wave per SIMD (their state spills past 256
 // VGPRs into AGPRs instead of scratch: __launch_bounds__ above), shorter ones 2.  (C = 3 at 2
 // waves per SIMD spilled 12 B to scratch; 1024 walks at N = 150, 32 lanes at one wave per
 // SIMD: 10.2 → 6.2 ms, profiles/r5q/.)
@@ -701,7 +703,7 @@ int lanes_per_instance(const zmpc_plan* p, int64_t ninst) {
   const int64_t cus = p->cus > 0 ? p->cus : 256;
   // (one instance per SIMD: at N ≤ 128 the whole-wave instances would fit two waves per SIMD,
   // but two instances per wave already run 1.6–1.8× faster there, profiles/r5t/)
-  return (ninst > cus * 4 && p->N <= 512) ? 32 : 64;
+  return (ninst > cus * 4 && p->N <= kScan32MaxN) ? 32 : 64;
 }
 
 hipError_t launch(const zmpc_plan* p, const ScanArgs& a, hipStream_t s, int L) {
@@ -733,7 +735,8 @@ hipError_t launch(const zmpc_plan* p, const ScanArgs& a, hipStream_t s, int L) {
     hipLaunchKernelGGL((zmpc_strict_scan_kernel<CC, 64>), grid, blk, 0, s, a); \
     break;
     ZMPC_SCASE(1) ZMPC_SCASE(2) ZMPC_SCASE(3) ZMPC_SCASE(4) ZMPC_SCASE(5) ZMPC_SCASE(6)
-    ZMPC_SCASE(7) ZMPC_SCASE(8)
+    ZMPC_SCASE(7) ZMPC_SCASE(8) ZMPC_SCASE(9) ZMPC_SCASE(10) ZMPC_SCASE(11) ZMPC_SCASE(12)
+    ZMPC_SCASE(13) ZMPC_SCASE(14) ZMPC_SCASE(15)
 #undef ZMPC_SCASE
     default:
       return hipErrorInvalidValue;
@@ -743,7 +746,7 @@ hipError_t launch(const zmpc_plan* p, const ScanArgs& a, hipStream_t s, int L) {
 
 }  // namespace
 
-bool zmpc_strict_scan_supported(const zmpc_plan* p) { return p->N >= 1 && p->N <= 512; }
+bool zmpc_strict_scan_supported(const zmpc_plan* p) { return p->N >= 1 && p->N <= kScanMaxN; }
 
 hipError_t zmpc_launch_rollout_strict_scan(const zmpc_plan* p, int64_t B, int64_t n,
                                            const double* zmax, const double* zmin,
@@ -752,7 +755,7 @@ hipError_t zmpc_launch_rollout_strict_scan(const zmpc_plan* p, int64_t B, int64_
                                            double* hist, int32_t* status, hipStream_t s,
                                            std::string* why) {
   if (!zmpc_strict_scan_supported(p)) {
-    *why = "the small-batch strict kernel supports horizons N <= 512";
+    *why = "the small-batch strict kernel supports horizons N <= 960";
     return hipErrorInvalidValue;
   }
   if (status) {
@@ -784,7 +787,7 @@ hipError_t zmpc_launch_step_strict_scan(const zmpc_plan* p, int64_t B, const dou
                                         double* x_next, int32_t* status, hipStream_t s,
                                         std::string* why) {
   if (!zmpc_strict_scan_supported(p)) {
-    *why = "the small-batch strict kernel supports horizons N <= 512";
+    *why = "the small-batch strict kernel supports horizons N <= 960";
     return hipErrorInvalidValue;
   }
   if (B == 0) return hipSuccess;

@@ -913,12 +913,16 @@ def test_strict_long_horizon_rollout_vs_oracle():
     assert np.abs(h[:, 1] - d["n400_yhist"]).max() <= 1e-6
 
 
-@pytest.mark.parametrize("N", (400, 700, 1300))
-def test_strict_long_horizon_step_vs_oracle(N):
-    """Cold-start strict solves at horizons run with 4, 2 and 1 waves per workgroup, vs the
-    reference's own strict calls (strict_long_ref.npz)."""
+@pytest.mark.parametrize("N,solver", ((400, 3), (400, 4), (700, 3), (700, 4), (1300, 0)))
+def test_strict_long_horizon_step_vs_oracle(N, solver):
+    """Cold-start strict solves, vs the reference's own strict calls (strict_long_ref.npz): the
+    LQ kernel (3) at horizons it runs with 4, 2 and 1 waves per workgroup, the parallel-in-time
+    kernel (4) with whole-wave instances to N = 960 (C = 7 and 11 slots per lane), and the
+    automatic choice beyond it (N = 1300: the LQ kernel)."""
     d = golden("strict_long_ref.npz")
     p = plan(N, strict=True)
+    if solver:
+        p.set_option("strict_solver", solver)
     out, st = p.step(d[f"step{N}_x"], d[f"step{N}_zmax"], d[f"step{N}_zmin"])
     ref = d[f"step{N}_out"]
     assert int(st.abs().max()) == 0
@@ -963,9 +967,12 @@ def test_strict_solvers_vs_reference(solver):
     out, st = p.step(lg["step400_x"], lg["step400_zmax"], lg["step400_zmin"])
     ref = lg["step400_out"]
     assert np.abs(out.cpu().numpy() - ref).max() <= 1e-7 * max(1.0, np.abs(ref).max())
-    if solver in (1, 2, 4):
+    if solver in (1, 2):
         with pytest.raises(ValueError, match="reduced-Cholesky"):
             plan(600, strict=True).set_option("strict_solver", solver)
+    if solver == 4:
+        with pytest.raises(ValueError, match="small-batch"):
+            plan(961, strict=True).set_option("strict_solver", solver)
 
 
 @pytest.mark.parametrize("solver", (3, 4))
@@ -1044,13 +1051,15 @@ def test_strict_small_and_large_batch_paths_agree(B, auto):
 
 @pytest.mark.parametrize("N,B", ((1, 3), (2, 5), (63, 7), (65, 7), (20, 600), (40, 600),
                                  (129, 1100), (257, 5), (300, 600), (400, 600), (512, 3),
-                                 (512, 600)))
+                                 (512, 600), (513, 3), (700, 1100), (960, 2)))
 def test_strict_scan_kernel_chunk_widths(N, B):
-    """The parallel-in-time kernel at the edges of its chunk widths (C = ⌈N/64⌉ = 1..8 slots
-    per lane; N = 65/129 leave the last lane one slot, N = 1 a single lane) and with 32 lanes per
+    """The parallel-in-time kernel at the edges of its chunk widths (C = ⌈N/64⌉ = 1..15 slots
+    per lane; N = 65/129/513 leave the last lane one slot, N = 1 a single lane, N = 960 the
+    widest whole-wave chunk) and with 32 lanes per
     instance (beyond one instance per SIMD: B = 600 walks at N = 20 / 40, 1 and 2 slots per lane
     of 32; B = 1100 at N = 129; B = 600 at N = 300 / 400 / 512: 10 / 13 / 16 slots per lane of
-    32) against the LQ kernel on
+    32; past N = 512 whole waves again, B = 1100 at N = 700 in two dispatch rounds) against the
+    LQ kernel on
     the same kicked walks: CoM within 1e-9, same statuses; and one window-mode step."""
     zmax, zmin, x0, F, dt = synthetic_batch(B, 64 if N < 150 else 150, seed=N)
     n = zmax.shape[1]
