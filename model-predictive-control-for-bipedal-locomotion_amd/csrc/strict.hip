@@ -34,7 +34,7 @@ typedef double dbl4 __attribute__((ext_vector_type(4)));
 constexpr int SNB = 16;            // instances per tile (= MFMA column tile)
 constexpr int SWAVES = 4;          // waves per workgroup
 constexpr int SPW = SNB / SWAVES;  // instances per wave
-constexpr int SMAXIT = 64;         // PDAS iteration cap
+constexpr int SMAXIT = 1024;       // PDAS iteration cap (as strict_lq.hip)
 
 struct StrictArgs {
   int N, Np, ld;         // horizon, padded to 16, W/D leading dimension

@@ -58,7 +58,10 @@ namespace {
 
 using namespace zmpc_eta;
 
-constexpr int LQ_MAXIT = 64;  // active-set pass cap (as strict.hip)
+// active-set pass cap (as strict.hip).  64 was too few: at (Q, R, h) = (0.1, 1e-3, 0.5) and
+// N = 400 the reference's exact answer takes 150 primal-dual passes from a cold start and 212
+// after an 800 N kick (strict_weights_long_ref.npz); the cap only bounds a cycling iteration
+constexpr int LQ_MAXIT = 1024;
 #ifdef ZMPC_DIAG
 constexpr bool kLqProf = true;  // per-phase clocks (ZMPC_LQ_PROF), diagnostics build only
 #else

@@ -43,7 +43,7 @@ namespace {
 
 using namespace zmpc_eta;
 
-constexpr int SC_MAXIT = 64;  // active-set pass cap (as strict_lq.hip)
+constexpr int SC_MAXIT = 1024;  // active-set pass cap (as strict_lq.hip)
 // horizons of the kernel: 32-lane instances to N = 512 (C ≤ 16 slots per lane: 256 VGPRs + 248
 // AGPRs), whole-wave ones to 960 (C ≤ 15: 256 + 236; C = 16 of 64 lanes spills 12 B to scratch)
 constexpr int kScan32MaxN = 512;

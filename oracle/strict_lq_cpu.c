@@ -28,7 +28,7 @@
 #include <stdlib.h>
 #include <string.h>
 
-#define LQ_MAXIT 64
+#define LQ_MAXIT 1024  // (as strict_lq.hip)
 #define ST_MAXITER 1
 #define ST_NONFINITE 2
 

@@ -33,6 +33,8 @@ Saved (tests/golden/strict_ref.npz):
 
 Usage: PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_strict_ref_golden.py          → strict_ref.npz
        PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_strict_ref_golden.py --long   → strict_long_ref.npz
+       PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_strict_ref_golden.py --weights-long
+                                                                    → strict_weights_long_ref.npz
 """
 import contextlib
 import io
@@ -471,9 +473,100 @@ def main_weights():
     print("saved", os.path.join(HERE, "strict_weights_ref.npz"))
 
 
+def main_weights_long():
+    """Non-default weights at long horizons → strict_weights_long_ref.npz.  Per point w
+    (WEIGHT_POINTS[w]):
+    * w{w}_n400_*: 200 samples of the default walk's stepping phase at horizon 400 (reference
+      CoPGenerator, rows 100..299) from rest at the first CoP centre, generate_com_trajectory
+      with an 800 N kick at n//2 (as main_long()'s n400 case);
+    * w{w}_step700_*: 8 cold predict_wieber_axis calls at horizon 700 with heavily active
+      bounds."""
+    sys.modules["cvxpy"] = make_cp()
+    sys.dont_write_bytecode = True
+    sys.path.insert(0, REF)
+    from src.mpc_bipedal.config import MPCConfig
+    from src.mpc_bipedal.generators import CoPGenerator
+    from src.mpc_bipedal.controllers import ZMPController
+
+    def instrument(ctl):
+        orig = ctl.predict_wieber_axis
+
+        def record(x_init, nb_steps, z_max, z_min):
+            _Rec.call = (np.array(x_init, np.float64), nb_steps, np.array(z_max), np.array(z_min),
+                         ctl.config)
+            out = orig(x_init, nb_steps, z_max, z_min)
+            _Rec.axis ^= 1
+            return out
+        ctl.predict_wieber_axis = record
+        return ctl
+
+    out = {"weights": np.array(WEIGHT_POINTS)}
+    dev = 0.0
+    rng = np.random.default_rng(20261018)
+    for w, (Qv, Rv, hv, gv) in enumerate(WEIGHT_POINTS):
+        N = 400
+        d = default_mpc_dict()
+        d.update(horizon=N, strict=True, add_force=True, F_ext=800.0, Q=Qv, R=Rv, h=hv, g=gv)
+        cfg = MPCConfig(**d)
+        zmax, zmin, _ = CoPGenerator(cfg).generate_cop_trajectory(save_footsteps=False)
+        zx, zn = zmax[100:300].copy(), zmin[100:300].copy()
+        n = len(zx)
+        mid = (zx[0] + zn[0]) / 2
+        x0 = np.array([mid[0], 0.0, 0.0])
+        y0 = np.array([mid[1], 0.0, 0.0])
+        ctl = instrument(ZMPController(cfg))
+        _Rec.rollout, _Rec.axis, _Rec.warm = True, 0, [None, None]
+        with contextlib.redirect_stdout(io.StringIO()), contextlib.redirect_stderr(io.StringIO()):
+            com, y_hist = ctl.generate_com_trajectory(x0.reshape(3, 1), y0.reshape(3, 1), zx, zn)
+        kick = cfg.dt * cfg.F_ext / cfg.m
+        ref = O.rollout_strict(x0, y0, zx, zn, N, cfg.dt, hv, gv, Qv, Rv, kick=kick,
+                               kick_step=n // 2)
+        e = max(float(np.abs(ref[:, :, 0] - com).max()),
+                float(np.abs(ref[:, 1] - y_hist[:, :, 0]).max()))
+        dev = max(dev, e)
+        out.update({f"w{w}_n400_zmax": zx, f"w{w}_n400_zmin": zn, f"w{w}_n400_x0": x0,
+                    f"w{w}_n400_y0": y0, f"w{w}_n400_kick": kick, f"w{w}_n400_com": com,
+                    f"w{w}_n400_yhist": y_hist[:, :, 0]})
+        print(f"w{w} (Q={Qv:g}, R={Rv:g}, h={hv:g}, g={gv:g}) N=400: rollout vs oracle "
+              f"max |d| {e:.2e}, {_Rec.n_qp} QPs", flush=True)
+        _Rec.rollout = False
+        N, B = 700, 8
+        d = default_mpc_dict()
+        d.update(horizon=N, strict=True, Q=Qv, R=Rv, h=hv, g=gv)
+        ctl = instrument(ZMPController(MPCConfig(**d)))
+        x = np.stack([rng.uniform(-0.05, 0.05, B), rng.uniform(-0.6, 0.6, B),
+                      rng.uniform(-6, 6, B)], 1)
+        ctr = rng.uniform(-0.05, 0.05, (B, 1)) + np.cumsum(
+            rng.normal(0, 0.003 * np.sqrt(150 / N), (B, N)), 1)
+        zmax_w = ctr + rng.uniform(0.005, 0.06, (B, N))
+        zmin_w = ctr - rng.uniform(0.005, 0.06, (B, N))
+        res = np.stack([ctl.predict_wieber_axis(x[b].reshape(3, 1), N, zmax_w[b].reshape(N, 1),
+                                                zmin_w[b].reshape(N, 1)).ravel()
+                        for b in range(B)])
+        e = float(np.abs(res - O.strict_step_batch(x, zmax_w, zmin_w, N, 1.5 / N, hv, gv, Qv,
+                                                   Rv)).max())
+        dev = max(dev, e)
+        out[f"w{w}_step700_x"], out[f"w{w}_step700_zmax"] = x, zmax_w
+        out[f"w{w}_step700_zmin"], out[f"w{w}_step700_out"] = zmin_w, res
+        print(f"w{w} step N=700: {B} cold calls, vs oracle max |d| {e:.2e}", flush=True)
+    print(f"{_Rec.n_qp} captured QPs; max rel problem diff {_Rec.max_rel:.2e}; KKT {_Rec.kkt}")
+    assert _Rec.max_rel <= 1e-13, _Rec.max_rel
+    assert _Rec.kkt["primal"] <= 1e-13 and _Rec.kkt["stationarity"] <= 1e-10, _Rec.kkt
+    assert dev <= 1e-12, dev
+    out["max_rel_problem_diff"] = _Rec.max_rel
+    out["kkt_worst"] = np.array([_Rec.kkt[k] for k in ("primal", "stationarity", "dual_hi",
+                                                         "dual_lo")])
+    out["max_abs_vs_oracle"] = dev
+    out["n_qps"] = _Rec.n_qp
+    np.savez_compressed(os.path.join(HERE, "strict_weights_long_ref.npz"), **out)
+    print("saved", os.path.join(HERE, "strict_weights_long_ref.npz"))
+
+
 if __name__ == "__main__":
     if "--long" in sys.argv:
         main_long()
+    elif "--weights-long" in sys.argv:
+        main_weights_long()
     elif "--weights" in sys.argv:
         main_weights()
     else:

@@ -1012,6 +1012,38 @@ def test_strict_weights_vs_reference(w, solver):
         assert np.abs(out.cpu().numpy() - ref).max() <= 1e-9 * max(1.0, np.abs(ref).max()), N
 
 
+@pytest.mark.parametrize("solver", (3, 4))
+@pytest.mark.parametrize("w", range(5))
+def test_strict_weights_long_horizon(w, solver):
+    """The five (Q, R, h, g) points of test_strict_weights_vs_reference at long horizons
+    (tests/golden/strict_weights_long_ref.npz, make_strict_ref_golden.py --weights-long): the
+    reference's strict branch on 200 samples of the default walk's stepping phase at N = 400 with
+    an 800 N kick, and 8 cold heavily-active calls at N = 700.  Both kernels (3: the LQ kernel
+    with 4-wave workgroups at N = 400, 2 at 700; 4: whole-wave scan instances, 7 and 11 slots
+    per lane): CoM RMSE ≤ 1e-9 and single solves ≤ 1e-7 relative, as the default-weight long
+    fixtures (test_strict_long_horizon_*), every status 0."""
+    d = golden("strict_weights_long_ref.npz")
+    Qv, Rv, hv, gv = (float(v) for v in d["weights"][w])
+    N = 400
+    zx, zn = d[f"w{w}_n400_zmax"], d[f"w{w}_n400_zmin"]
+    n = len(zx)
+    p = Plan(torch.cuda.current_device(), N, 1.5 / N, hv, gv, Qv, Rv, True)
+    p.set_option("strict_solver", solver)
+    x0 = np.stack([d[f"w{w}_n400_x0"], d[f"w{w}_n400_y0"]])[None]
+    h, st = p.rollout(zx, zn, x0, kick=np.array([float(d[f"w{w}_n400_kick"])]), kick_step=n // 2)
+    assert int(st.abs().max()) == 0
+    h = h.cpu().numpy()[0]
+    assert rmse(h[:, :, 0], d[f"w{w}_n400_com"]) <= 1e-9
+    assert np.abs(h[:, 1] - d[f"w{w}_n400_yhist"]).max() <= 1e-6
+    N = 700
+    p = Plan(torch.cuda.current_device(), N, 1.5 / N, hv, gv, Qv, Rv, True)
+    p.set_option("strict_solver", solver)
+    out, st = p.step(d[f"w{w}_step700_x"], d[f"w{w}_step700_zmax"], d[f"w{w}_step700_zmin"])
+    ref = d[f"w{w}_step700_out"]
+    assert int(st.abs().max()) == 0
+    assert np.abs(out.cpu().numpy() - ref).max() <= 1e-7 * max(1.0, np.abs(ref).max())
+
+
 @pytest.mark.parametrize("w", (0, 2))
 def test_strict_weights_drop_in(w):
     """The drop-in at non-default weights: ZMPController(MPCConfig(Q, R, h, g, strict=True))
