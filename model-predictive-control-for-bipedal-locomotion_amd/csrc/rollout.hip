@@ -1461,6 +1461,13 @@ struct WideGeom {
 #endif
 constexpr bool kWide8 = ZMPC_WIDE8 != 0;
 
+// The wide kernel's dynamic-LDS ceiling: 64 KiB (the 4-waves-per-SIMD bound leaves no room above
+// it for W = 2 and 4), but 159 KiB for W = 8 — a 16-wave workgroup fills a CU's wave slots at that
+// bound alone, so its LDS costs no occupancy (walks of 2561..4096 samples at N >= 920 took the
+// chunk kernel at 8x the time, profiles/r6fin/configs/sweep_full.jsonl).  The kernel's static LDS
+// (≈0.5 KiB) comes on top: hipFuncSetAttribute refuses a dynamic limit of the full 160 KiB.
+size_t wide_lds_cap(int w) { return (size_t)(w == 8 ? 159 : 64) * 1024; }
+
 bool wide_geom(int N, int64_t n, WideGeom* g) {
   const int64_t ns = n - 1;
   // (449..512 timesteps: the single-pass split kernel's CW = 8 runs 1.7× slower per walk than
@@ -1472,8 +1479,7 @@ bool wide_geom(int N, int64_t n, WideGeom* g) {
   g->lz = g->w * 64 * g->cw + g->kc + 1;
   const int pad = (g->cw % 2 == 0) ? 1 : 0;
   g->lzp = ((g->lz + pad * (g->lz / g->cw) + 1) + 1) & ~1;
-  // default 64 KiB LDS cap (the 4-waves-per-SIMD bound leaves no room above it)
-  return (size_t)2 * g->lzp * sizeof(double) <= 64 * 1024;
+  return (size_t)2 * g->lzp * sizeof(double) <= wide_lds_cap(g->w);
 }
 
 // Walks of any length (the fallback beyond the wide kernel's 64·8·8 + 1 samples): one wave per
@@ -1736,6 +1742,13 @@ int occupancy(const void* kernel, int threads, size_t lds) {
 // profiles/r3pfw/).
 template <int C, int W, int E>
 void launch_wide(hipStream_t s, RolloutArgs q, size_t lds, int64_t B, int cus) {
+  if (lds > 64 * 1024) {  // (W = 8 only, wide_lds_cap): raise the kernel's dynamic-LDS limit
+    static size_t raised = 64 * 1024;
+    if (lds > raised &&
+        hipFuncSetAttribute(reinterpret_cast<const void*>(zmpc_rollout_unc_wide_kernel<C, W, E>),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) == hipSuccess)
+      raised = lds;
+  }
   const int occ = occupancy(reinterpret_cast<const void*>(zmpc_rollout_unc_wide_kernel<C, W, E>),
                             128 * W, lds);
   const int64_t R = (int64_t)std::max(cus, 1) * occ;
@@ -1939,7 +1952,7 @@ hipError_t zmpc_launch_rollout_unc(const zmpc_plan* p, int64_t B, int64_t n, con
     // the sparse attempt's table and change lists behind the z_ref areas (within the default
     // 64 KiB dynamic-LDS ceiling, else dense only)
     const size_t lds_sp = (2 * (size_t)wg.lzp + wide_sparse_doubles(p->N)) * sizeof(double);
-    if (q.ksum != nullptr && lds_sp <= 64 * 1024)
+    if (q.ksum != nullptr && lds_sp <= wide_lds_cap(wg.w))
       lds_w = std::max(lds_w, lds_sp);
     else
       q.ksum = nullptr;

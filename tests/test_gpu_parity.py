@@ -369,6 +369,29 @@ def test_chunk_kernel_equals_wide_kernel():
         assert np.abs(res[0] - res[1]).max() <= 1e-12
 
 
+@pytest.mark.parametrize("N,n", ((920, 2570), (700, 4097)))
+def test_wide_kernel_past_64k_lds(N, n):
+    """Walks whose wide-kernel geometry needs more than 64 KiB of LDS (8-wave axes, 75 / 86 KiB:
+    rollout.hip wide_lds_cap) take the wide kernel instead of the chunked one: equal to the
+    chunked kernel (ZMPC_OPT_LONG_WALK = 3) to 1e-12 and to the oracle to 1e-8."""
+    rng = np.random.default_rng(N + n)
+    dt = 1.5 / N
+    B = 3
+    ctr = np.cumsum(rng.normal(0, 0.004, (B, n, 2)), 1)
+    zmax, zmin = ctr + 0.05, ctr - 0.05
+    x0 = rng.normal(0, 0.01, (B, 2, 3))
+    kick = rng.uniform(0, 0.1, B)
+    res = []
+    for form in (0, 3):
+        p = plan(N, dt=dt).set_option("long_walk", form)
+        h, st = p.rollout(zmax, zmin, x0, kick=kick, kick_step=n // 2)
+        assert int(st.abs().max()) == 0
+        res.append(h.cpu().numpy())
+    assert np.abs(res[0] - res[1]).max() <= 1e-12
+    ref = O.rollout_gain(zmax, zmin, x0, N, dt, H, G, Q, R, kick, n // 2)
+    assert np.abs(res[0] - ref).max() <= 1e-8
+
+
 def test_kick_step_out_of_range_is_no_kick():
     zmax, zmin, x0, F, dt = synthetic_batch(8, 64)
     p = plan(64, dt=dt)
