@@ -811,6 +811,11 @@ def main():
                          "sub-record (0 = no sub-record)")
     ap.add_argument("--strict-cpu-seconds", type=float, default=4.0,
                     help="CPU-leg budget per process of the strict sub-record")
+    ap.add_argument("--herdt-steps", type=int, default=3,
+                    help="default line (config 2): timed launches of the config-6 Herdt "
+                         "sub-record (0 = no sub-record)")
+    ap.add_argument("--herdt-cpu-seconds", type=float, default=4.0,
+                    help="CPU-leg budget per process of the Herdt sub-record")
     ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
                     help="plan option (mpc_bipedal/_native.py OPTIONS, include/zmpc.h "
                          "ZMPC_OPT_*) for A/B timing of forms with the same results")
@@ -869,6 +874,11 @@ def main():
             sub = strict_subrecord(args, rank, world, dev, dist_on)
             if rank == 0:
                 line["strict"] = sub
+        if conf == 2 and args.herdt_steps > 0 and not args.batch and not args.horizon:
+            # the Herdt experiment (zmp_controller.py:435-826, config 6) likewise
+            sub = herdt_subrecord(args, rank, world, dev, dist_on)
+            if rank == 0:
+                line["herdt"] = sub
     if rank == 0:
         print(json.dumps(line))
     if dist_on:
@@ -889,6 +899,22 @@ def strict_subrecord(args, rank, world, dev, dist_on):
     if rank != 0:
         return None
     for k in ("metric", "higher_is_better", "vs_baseline", "correlation", "pipelined"):
+        sub.pop(k, None)
+    return sub
+
+
+def herdt_subrecord(args, rank, world, dev, dist_on):
+    """Config 6 (32 768 Herdt walks per GPU, N = 150, f64) as a second sub-record of the default
+    line, built like `strict_subrecord`: its own warm-up and timed region, roofline and, at one
+    GPU, the CPU legs with a shorter budget."""
+    sa = argparse.Namespace(**vars(args))
+    sa.steps, sa.warmup = args.herdt_steps, 1
+    sa.batch, sa.horizon = None, None
+    sa.cpu_seconds = args.herdt_cpu_seconds
+    sub = herdt_bench(sa, rank, world, dev, dist_on)
+    if rank != 0:
+        return None
+    for k in ("metric", "higher_is_better", "vs_baseline"):
         sub.pop(k, None)
     return sub
 
