@@ -1333,22 +1333,7 @@ __global__ void __launch_bounds__(128 * W, E == 4 ? 6 : 4) zmpc_rollout_unc_wide
     matvec3(P, xi, t);
     for (int i = 0; i < 3; ++i) sv[i] += t[i];
   }
-#pragma unroll
-  for (int r2 = 0; r2 < 6; ++r2) {
-    const int d = 1 << r2;
-    if (dbgb(a, 2)) break;
-    double u[3];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) u[i] = __shfl_up(sv[i], d, 64);
-    if (lane >= d) {
-      Mat3 Pd;
-#pragma unroll
-      for (int q = 0; q < 9; ++q) Pd.m[q] = Pp[r2 * 9 + q];
-      double t[3];
-      matvec3(Pd, u, t);
-      for (int i = 0; i < 3; ++i) sv[i] += t[i];
-    }
-  }
+  if (!dbgb(a, 2)) scan_dpp(sv, lane, Pp, a.scanP + kScanPowOff + (CW - 1) * 33 * 9);
   if (lane == 63) {
     send[axis][w][0] = sv[0];
     send[axis][w][1] = sv[1];
@@ -1384,7 +1369,7 @@ __global__ void __launch_bounds__(128 * W, E == 4 ? 6 : 4) zmpc_rollout_unc_wide
   double xs0[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
-    const double p = __shfl_up(sv[i], 1, 64);
+    const double p = dpp_f64<0x138, 0xF>(sv[i]);  // wave_shr:1
     xs0[i] = (lane == 0) ? xs[i] : p;
   }
   tl_stamp(a, b, 3);
