@@ -1351,20 +1351,28 @@ __global__ void __launch_bounds__(128 * W, E == 4 ? 6 : 4) zmpc_rollout_unc_wide
       matvec3(M64, xs, t);
       for (int i = 0; i < 3; ++i) xs[i] = send[axis][v][i] + t[i];
     }
+    // lane l adds (Ā^CW)^(l+1)·x_start: the plan's per-lane powers k ≤ 32, times (Ā^CW)^32
+    // (scan level 5) first for lanes 32..63
     double vv[3] = {xs[0], xs[1], xs[2]};
-    const int e = lane + 1;
+    int e = lane + 1;
+    if (e > 32) {
+      Mat3 P32;
 #pragma unroll
-    for (int r2 = 0; r2 < 7; ++r2) {
-      if ((e >> r2) & 1) {
-        Mat3 Pd;
-#pragma unroll
-        for (int q = 0; q < 9; ++q) Pd.m[q] = Pp[r2 * 9 + q];
-        double t[3];
-        matvec3(Pd, vv, t);
-        for (int i = 0; i < 3; ++i) vv[i] = t[i];
-      }
+      for (int q = 0; q < 9; ++q) P32.m[q] = Pp[5 * 9 + q];
+      double t[3];
+      matvec3(P32, vv, t);
+      for (int i = 0; i < 3; ++i) vv[i] = t[i];
+      e -= 32;
     }
-    for (int i = 0; i < 3; ++i) sv[i] += vv[i];
+    {
+      const double* m = a.scanP + kScanPowOff + ((CW - 1) * 33 + e) * 9;
+      Mat3 M;
+#pragma unroll
+      for (int q = 0; q < 9; ++q) M.m[q] = m[q];
+      double t[3];
+      matvec3(M, vv, t);
+      for (int i = 0; i < 3; ++i) sv[i] += t[i];
+    }
   }
   double xs0[3];
 #pragma unroll
