@@ -1226,13 +1226,29 @@ __global__ void __launch_bounds__(128 * W, E == 4 ? 6 : 4) zmpc_rollout_unc_wide
     if (a.ksum != nullptr) {
       const double2* zmx = reinterpret_cast<const double2*>(a.zmax + b * a.bstride);
       const double2* zmn = reinterpret_cast<const double2*>(a.zmin + b * a.bstride);
-      const int lzs = W * 64 * CW + 1;
-      for (int i = tid; i < ksum_rows(a.hN); i += NT) Ts[i] = a.ksum[i];
-      for (int t = tid; t < lzs; t += NT) {
-        const int tc = min(t, n - 1);  // padding = last row
-        const double2 hi = zmx[tc], lo = zmn[tc];
-        zr0[ZL::idx(t)] = (hi.x + lo.x) / 2;
-        zr1[ZL::idx(t)] = (hi.y + lo.y) / 2;
+      // the bound loads issued GB rows per thread at a time ahead of their LDS stores (one HBM
+      // round trip per group instead of per row; two-row groups at CW ≥ 7, whose state would
+      // spill at four)
+      constexpr int lzs = W * 64 * CW + 1, IT = (lzs + NT - 1) / NT, GB = CW >= 7 ? 2 : 4;
+#pragma unroll
+      for (int u0 = 0; u0 < IT; u0 += GB) {
+        double2 hi[GB], lo[GB];
+#pragma unroll
+        for (int u = 0; u < GB; ++u) {
+          const int tc = min(tid + (u0 + u) * NT, n - 1);  // padding = last row
+          hi[u] = zmx[tc];
+          lo[u] = zmn[tc];
+        }
+        if (u0 == 0)
+          for (int i = tid; i < ksum_rows(a.hN); i += NT) Ts[i] = a.ksum[i];
+#pragma unroll
+        for (int u = 0; u < GB; ++u) {
+          const int t = tid + (u0 + u) * NT;
+          if (u0 + u < IT && t < lzs) {
+            zr0[ZL::idx(t)] = (hi[u].x + lo[u].x) / 2;
+            zr1[ZL::idx(t)] = (hi[u].y + lo[u].y) / 2;
+          }
+        }
       }
       __syncthreads();
       tl_stamp(a, b, 1);
@@ -1333,7 +1349,29 @@ __global__ void __launch_bounds__(128 * W, E == 4 ? 6 : 4) zmpc_rollout_unc_wide
     matvec3(P, xi, t);
     for (int i = 0; i < 3; ++i) sv[i] += t[i];
   }
-  if (!dbgb(a, 2)) scan_dpp(sv, lane, Pp, a.scanP + kScanPowOff + (CW - 1) * 33 * 9);
+  // (the 6-waves-per-SIMD FFT instances at CW ≥ 7 keep the shuffle scan and binary powering:
+  // the DPP scan's per-lane powers would spill them, 12–36 B)
+  constexpr bool kShflScan = E == 4 && CW >= 7;
+  if constexpr (kShflScan) {
+#pragma unroll
+    for (int r2 = 0; r2 < 6; ++r2) {
+      const int d = 1 << r2;
+      if (dbgb(a, 2)) break;
+      double u[3];
+#pragma unroll
+      for (int i = 0; i < 3; ++i) u[i] = __shfl_up(sv[i], d, 64);
+      if (lane >= d) {
+        Mat3 Pd;
+#pragma unroll
+        for (int q = 0; q < 9; ++q) Pd.m[q] = Pp[r2 * 9 + q];
+        double t[3];
+        matvec3(Pd, u, t);
+        for (int i = 0; i < 3; ++i) sv[i] += t[i];
+      }
+    }
+  } else if (!dbgb(a, 2)) {
+    scan_dpp(sv, lane, Pp, a.scanP + kScanPowOff + (CW - 1) * 33 * 9);
+  }
   if (lane == 63) {
     send[axis][w][0] = sv[0];
     send[axis][w][1] = sv[1];
@@ -1355,16 +1393,29 @@ __global__ void __launch_bounds__(128 * W, E == 4 ? 6 : 4) zmpc_rollout_unc_wide
     // (scan level 5) first for lanes 32..63
     double vv[3] = {xs[0], xs[1], xs[2]};
     int e = lane + 1;
-    if (e > 32) {
-      Mat3 P32;
+    if constexpr (kShflScan) {  // binary powering over the scan levels
 #pragma unroll
-      for (int q = 0; q < 9; ++q) P32.m[q] = Pp[5 * 9 + q];
-      double t[3];
-      matvec3(P32, vv, t);
-      for (int i = 0; i < 3; ++i) vv[i] = t[i];
-      e -= 32;
-    }
-    {
+      for (int r2 = 0; r2 < 7; ++r2) {
+        if ((e >> r2) & 1) {
+          Mat3 Pd;
+#pragma unroll
+          for (int q = 0; q < 9; ++q) Pd.m[q] = Pp[r2 * 9 + q];
+          double t[3];
+          matvec3(Pd, vv, t);
+          for (int i = 0; i < 3; ++i) vv[i] = t[i];
+        }
+      }
+      for (int i = 0; i < 3; ++i) sv[i] += vv[i];
+    } else {
+      if (e > 32) {
+        Mat3 P32;
+#pragma unroll
+        for (int q = 0; q < 9; ++q) P32.m[q] = Pp[5 * 9 + q];
+        double t[3];
+        matvec3(P32, vv, t);
+        for (int i = 0; i < 3; ++i) vv[i] = t[i];
+        e -= 32;
+      }
       const double* m = a.scanP + kScanPowOff + ((CW - 1) * 33 + e) * 9;
       Mat3 M;
 #pragma unroll
@@ -1377,7 +1428,7 @@ __global__ void __launch_bounds__(128 * W, E == 4 ? 6 : 4) zmpc_rollout_unc_wide
   double xs0[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
-    const double p = dpp_f64<0x138, 0xF>(sv[i]);  // wave_shr:1
+    const double p = kShflScan ? __shfl_up(sv[i], 1, 64) : dpp_f64<0x138, 0xF>(sv[i]);
     xs0[i] = (lane == 0) ? xs[i] : p;
   }
   tl_stamp(a, b, 3);

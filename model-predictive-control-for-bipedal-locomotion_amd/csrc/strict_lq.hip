@@ -1257,8 +1257,11 @@ struct LqVariant {
   zmpc_strict_lq_kernel<LQ_S, G, false, false, Q>, zmpc_strict_lq_kernel<LQ_S, G, true, false, Q>, \
       zmpc_strict_lq_kernel<LQ_S, G, false, true, Q>, zmpc_strict_lq_kernel<LQ_S, G, true, true, Q>
 #define ZMPC_LQV(G) {G, ZMPC_LQK(G, false), nullptr, nullptr, nullptr, nullptr}
+// (The queue form exists for run-length bounds only: with the bounds staged one row per sample,
+// ZMPC_OPT_STRICT_BOUNDS = 1, its instances spill 20 B — those launches take the one-round form.)
 const LqVariant kLqVariants[] = {
-    {8, ZMPC_LQK(8, false), ZMPC_LQK(8, true)},  // default
+    {8, ZMPC_LQK(8, false), nullptr, nullptr, zmpc_strict_lq_kernel<LQ_S, 8, false, true, true>,
+     zmpc_strict_lq_kernel<LQ_S, 8, true, true, true>},  // default
     ZMPC_LQV(4),  // N up to 2176 (the default G = 8: up to 896)
     ZMPC_LQV(2),  // N up to 2464 (ZMPC_STRICT_MAX_N)
 };
