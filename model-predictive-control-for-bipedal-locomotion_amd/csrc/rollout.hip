@@ -835,7 +835,7 @@ __device__ __forceinline__ void split_walk(const RolloutArgs& a, int64_t b, doub
   double x[3];
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
-    const double p = __shfl_up(sv[i], 1, 64);
+    const double p = dpp_f64<0x138, 0xF>(sv[i]);  // wave_shr:1
     x[i] = (lane == 0) ? xi[i] : p;
   }
   // ---- 5. replay (reference form) straight into the staged history ------------------------
